@@ -1,0 +1,209 @@
+"""bench.py — decoded tokens/s of int8 greedy decode on MI355X (BASELINE.json metric).
+
+    python bench.py --gpus N --steps K --warmup W
+
+One "step" = one whole greedy decode of one batch of synthetic sentences: encoder, cross
+K/V, max_len-1 = 71 KV-cached decoder steps, generator + argmax (the fixed loop of
+reference/onnx_reference_inference.py:630, no EOS exit).  Workload at N=1 = BASELINE
+config 2: batch 32 per GPU, source length <= 64 padded to 72.  For N > 1 each rank (one
+process per GPU, torchrun) decodes its own 32-sentence shard with its own weight replica:
+weak scaling, no collective on the data path; RCCL is used only for the
+barrier and the max-over-ranks of the elapsed time.
+
+Printed JSON (rank 0) adds:
+  roofline     dominant kernel, algorithmic bytes per launch / measured avg duration
+  cpu_baseline the numpy oracle (CPU restatement, "port") on a bounded sample, rank 0 only
+  cfg3_encoder encoder-only B=256 S=128 QuantLinear int8 ops/s vs the MFMA int8 peak
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "onnx-transformer_amd"))
+
+PEAK_INT8_OPS = 256 * 4096 * 2 * 2.4e9     # dense int8 MFMA: 5.03e15 ops/s (MI355X_MICROARCH.md)
+PEAK_HBM = 8.0e12                           # bytes/s (spec)
+D, F = 512, 2048
+
+
+def make_src(rng, B, S, max_src=64):
+    """BOS + uniform tokens + EOS, lengths uniform in [8, max_src], padded with <blank>=2."""
+    src = np.full((B, S), 2, np.int64)
+    lens = rng.integers(8, max_src + 1, B)
+    for b, n in enumerate(lens):
+        src[b, 0] = 0
+        src[b, 1:n - 1] = rng.integers(4, 5337, n - 2)
+        src[b, n - 1] = 1
+    return src, lens
+
+
+def encoder_gemm_ops(B, S, n_layers=6):
+    M = B * S
+    return n_layers * 2 * M * (3 * D * D + D * D + D * F + F * D)
+
+
+def time_kernel_decode_ffn1(model, B, iters=200):
+    """Dominant decode kernel: FFN1 GEMM at M=B (N=2048, K=512) on the model's weights.
+    Returns average duration (s) measured with HIP events on the launch stream."""
+    import ctypes as C
+
+    import torch
+
+    from qtx import _lib
+    rng = np.random.default_rng(1)
+    a8 = torch.from_numpy(rng.integers(-127, 128, (B, D)).astype(np.int8)).cuda()
+    sa = torch.full((B,), 0.01, device="cuda")
+    out = torch.empty((B, F), device="cuda")
+    w = torch.from_numpy(rng.integers(-127, 128, (F, D)).astype(np.int8)).cuda()
+    sw = torch.full((F,), 0.01, device="cuda")
+    bias = torch.zeros(F, device="cuda")
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = lambda t: C.c_void_p(t.data_ptr())
+    args = (P(a8), P(sa), P(w), P(sw), P(bias), B, F, D, 8, 1, C.c_void_p(0), P(out), st)
+    for _ in range(20):
+        _lib.call("qtx_linear_i8", *args)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        _lib.call("qtx_linear_i8", *args)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / iters
+
+
+def cpu_baseline(sd, B=4, S=72, max_len=72, seed=7):
+    """Numpy oracle greedy decode (KV cached) on a bounded sample, on this host's cores."""
+    from oracle.qtx_oracle import OracleModel
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        threads = os.cpu_count() or 1
+    om = OracleModel(sd)
+    src, _ = make_src(np.random.default_rng(seed), B, S)
+    mask = (src != 2)[:, None, :]
+    t0 = time.perf_counter()
+    om.greedy_decode(src, mask, max_len=max_len)
+    dt = time.perf_counter() - t0
+    return {"value": B * (max_len - 1) / dt, "unit": "decoded tokens/s", "cores": int(threads),
+            "kind": "port",
+            "sample": f"numpy oracle greedy decode, B={B} sentences, S={S}, {max_len - 1} steps, "
+                      f"KV-cached, {dt:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=32, help="sentences per GPU")
+    ap.add_argument("--src-len", type=int, default=72)
+    ap.add_argument("--max-len", type=int, default=72)
+    ap.add_argument("--weight-bits", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cfg3", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from qtx import _build
+    if rank == 0:
+        _build.build()
+    if world > 1:
+        dist.barrier()
+    from qtx.decode import greedy_decode
+    from qtx.model import QtxModel
+    from qtx.weights import ModelConfig, synthetic_state_dict
+
+    sd = synthetic_state_dict(20241223)
+    model = QtxModel(sd, ModelConfig(weight_bits=args.weight_bits))
+    B, S, L = args.batch, args.src_len, args.max_len
+    src, lens = make_src(np.random.default_rng(1000 + rank), B, S)
+    srcd = torch.from_numpy(src).cuda()
+    maskd = (srcd != 2).to(torch.uint8)
+    ids = torch.empty((B, L), dtype=torch.int64, device="cuda")
+
+    def step():
+        model.greedy(srcd, maskd, max_len=L, start=0, out=ids)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    tokens = world * B * (L - 1) * args.steps
+    value = tokens / dt
+
+    if rank == 0:
+        kt = time_kernel_decode_ffn1(model, B)
+        alg_bytes = F * D + B * D + B * 4 + F * 12 + B * F * 4   # W int8 + A + scales/bias + out f32
+        roof = {"kernel": f"k_gemm FFN1 decode (M={B}, N={F}, K={D}, int8)", "bound": "hbm",
+                "achieved": alg_bytes / kt / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                "frac": alg_bytes / kt / PEAK_HBM, "traffic": None, "avg_us": kt * 1e6,
+                "alg_bytes_per_launch": alg_bytes}
+        out = {"metric": "decoded tokens/sec IWSLT14 de-en int8 greedy (batch 32/GPU, 71 steps)",
+               "value": value, "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "int8" if args.weight_bits == 8 else "int4w-int8a",
+               "data": "synthetic (seeded src ids, random-init weights of the reference architecture)",
+               "config": {"workload": f"cfg2: greedy decode B={B}/GPU, src<=64 padded to {S}, "
+                                      f"max_len={L}", "global_batch": B * world, "seq_len": S,
+                          "parallelism": f"sentence-shard x{world}"},
+               "roofline": roof}
+        if not args.no_cfg3:
+            Bc, Sc = 256, 128
+            xs = torch.randn((Bc, Sc, D), device="cuda")
+            mk = torch.ones((Bc, Sc), dtype=torch.uint8, device="cuda")
+            for _ in range(2):
+                model.encode(xs, mk)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            n = 5
+            for _ in range(n):
+                model.encode(xs, mk)
+            e1.record()
+            torch.cuda.synchronize()
+            te = e0.elapsed_time(e1) / 1e3 / n
+            ops = encoder_gemm_ops(Bc, Sc)
+            out["cfg3_encoder"] = {"B": Bc, "S": Sc, "ms": te * 1e3,
+                                   "quantlinear_int8_ops": ops,
+                                   "whole_encoder_ops_per_s": ops / te,
+                                   "frac_of_int8_peak_whole_encoder": ops / te / PEAK_INT8_OPS}
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(sd)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

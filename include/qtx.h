@@ -1,0 +1,142 @@
+/* qtx.h — C-ABI of libqtx.so, the MI355X (gfx950) W8A8 transformer inference path.
+ *
+ * This library replaces the ONNXRuntime-CPU execution of the reference's exported
+ * encoder/decoder graphs (gebegebegebe/onnx-transformer).  Each entry point names the
+ * reference interface it stands in for:
+ *
+ *   qtx_encoder_forward  <- ort.InferenceSession('encoder_fixed.onnx').run(None,
+ *                           {global_in, global_in_1})       reference/onnx_reference_inference.py:625-626
+ *                           / run_module("encoder", ...)     onnx_optimized_inference.py:297-304
+ *   qtx_decoder_forward  <- InferenceSession('decoder_fixed.onnx').run(None, {global_in,
+ *                           global_in_1, global_in_2, global_in_3})
+ *                                                            reference/onnx_reference_inference.py:633-639
+ *   qtx_greedy_decode    <- greedy_decode(model, src, src_mask, max_len, start_symbol)
+ *                                                            reference/onnx_reference_inference.py:622-646
+ *                                                            (batched form batch_output.py:659-673)
+ *   qtx_embed            <- model.get_src_embed / get_tgt_embed  encoder_decoder.py:54-58
+ *   qtx_generator        <- model.generator(x) + torch.max     generator.py:14-15,
+ *                                                            reference/onnx_reference_inference.py:640-641
+ *   qtx_row_quant        <- quantize_activation_per_token_absmax / quantize_weight_per_channel_absmax
+ *                                                            quant_linear.py:30-43 / :5-17
+ *   qtx_layernorm_quant  <- LayerNorm.forward (+ the next W8A8Linear's act quant)
+ *                                                            layer_norm.py:12-15
+ *   qtx_linear_i8        <- W8A8Linear.forward (int8 GEMM + dequant epilogue) quant_linear.py:111-119
+ *   qtx_attention_i8     <- MultiHeadedAttention.attention     attention.py:23-36
+ *
+ * Conventions: every pointer is a DEVICE pointer (HIP, gfx950) unless the
+ * parameter says host; buffers are caller-owned; no entry point allocates device memory
+ * except qtx_model_create; `stream` is a hipStream_t (0 = default stream); every function
+ * returns 0 on success or a non-zero qtx_status, with a message in qtx_last_error().
+ * Thread-compatible: one stream per thread; the model handle is read-only after creation.
+ */
+#ifndef QTX_H_
+#define QTX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  QTX_OK = 0,
+  QTX_E_INVALID = 1,   /* bad argument / shape (the reference raises on shape mismatch) */
+  QTX_E_HIP = 2,       /* a HIP runtime error, message in qtx_last_error() */
+  QTX_E_WORKSPACE = 3, /* workspace too small: see qtx_*_workspace_size */
+  QTX_E_UNSUPPORTED = 4
+} qtx_status;
+
+typedef struct qtx_model qtx_model;
+
+/* make_model hyper-parameters (model.py:15-16).  d_model must be 512, d_ff a multiple of
+ * 256 up to 2048, n_heads * 64 == d_model.  weight_bits: 8 (W8A8) or 4 (packed int4). */
+typedef struct {
+  int32_t src_vocab, tgt_vocab, n_layers, d_model, d_ff, n_heads, max_len, weight_bits;
+} qtx_config;
+
+const char* qtx_last_error(void);
+const char* qtx_version(void);
+
+/* Number of float tensors qtx_model_create expects, and their names in order (the
+ * reference state_dict keys; see qtx/weights.py:tensor_order).  names may be NULL. */
+int32_t qtx_model_tensor_count(const qtx_config* cfg);
+
+/* Build the device-resident quantized model from fp32 DEVICE tensors given in
+ * tensor_order, plus the positional table pe [max_len, d_model].  Weights are quantized
+ * per output channel on the device (quant_linear.py:5-17).  The inputs may be freed after
+ * the call returns (it synchronizes `stream`). */
+int32_t qtx_model_create(const qtx_config* cfg, const float* const* tensors,
+                         int32_t n_tensors, const float* pe, void* stream, qtx_model** out);
+int32_t qtx_model_destroy(qtx_model* m);
+/* bytes of device memory owned by the model */
+size_t qtx_model_device_bytes(const qtx_model* m);
+
+/* Workspace sizes (bytes) for the model-level calls. */
+size_t qtx_encoder_workspace_size(const qtx_model* m, int32_t B, int32_t S);
+size_t qtx_decoder_workspace_size(const qtx_model* m, int32_t B, int32_t T, int32_t S);
+size_t qtx_greedy_workspace_size(const qtx_model* m, int32_t B, int32_t S, int32_t max_len);
+
+/* Encoder graph: x [B,S,d] fp32 (= src_embed(src), "global_in"), src_mask [B,S] uint8
+ * (nonzero = keep, "global_in_1" [B,1,S]) -> out [B,S,d] fp32 ("global_out"). */
+int32_t qtx_encoder_forward(const qtx_model* m, const float* x, const uint8_t* src_mask,
+                            int32_t B, int32_t S, float* out, void* ws, size_t ws_bytes,
+                            void* stream);
+
+/* Decoder graph: y [B,T,d] (= tgt_embed(ys), "global_in"), memory [B,S,d] ("global_in_1"),
+ * src_mask [B,S] uint8 ("global_in_2"), tgt_mask uint8 [T,T] or [B,T,T]
+ * (tgt_mask_batched = 0/1, "global_in_3") -> out [B,T,d] ("global_out"). */
+int32_t qtx_decoder_forward(const qtx_model* m, const float* y, const float* memory,
+                            const uint8_t* src_mask, const uint8_t* tgt_mask,
+                            int32_t tgt_mask_batched, int32_t B, int32_t T, int32_t S,
+                            float* out, void* ws, size_t ws_bytes, void* stream);
+
+/* Whole greedy decode: src ids int64 [B,S], src_mask uint8 [B,S] -> ids int64 [B,max_len]
+ * (ids[:,0] = start, then max_len-1 greedy steps with no EOS exit, like the reference).
+ * KV-cached; results equal the reference's full-prefix recompute (causal invariance). */
+int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t* src_mask,
+                          int32_t B, int32_t S, int32_t max_len, int64_t start, int64_t* ids,
+                          void* ws, size_t ws_bytes, void* stream);
+
+/* Embeddings + positional encoding: which = 0 (src) / 1 (tgt); ids int64 [B,T] ->
+ * out [B,T,d], positions pos0 .. pos0+T-1. */
+int32_t qtx_embed(const qtx_model* m, int32_t which, const int64_t* ids, int32_t B, int32_t T,
+                  int32_t pos0, float* out, void* stream);
+
+/* Generator: x [M,d] -> logp [M,tgt_vocab] (may be NULL), ids int64 [M] (first argmax).
+ * ws: M * tgt_vocab floats. */
+int32_t qtx_generator(const qtx_model* m, const float* x, int32_t M, float* logp,
+                      int64_t* ids, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- per-op entry points (parity tests, fault-injection hooks later) ---- */
+
+/* q[r,:] = rint(x[r,:] / s[r]), s[r] = max(max|x[r,:]|, 1e-5) / qmax.  D in {256,512,1024,2048}. */
+int32_t qtx_row_quant(const float* x, int32_t rows, int32_t D, float qmax, int8_t* q,
+                      float* s, void* stream);
+
+/* y = LN(x) (unbiased std, eps on std); optional fp32 y (may be NULL), optional q/s. */
+int32_t qtx_layernorm_quant(const float* x, const float* a, const float* b, int32_t rows,
+                            int32_t D, float* y, int8_t* q, float* s, void* stream);
+
+/* out[m,n] = ((float(sum_k A[m,k] W[n,k]) * sa[m]) * sw[n]) + bias[n], then
+ * flags: 1 = ReLU, 2 = residual (out = res + y).  weight_bits 8: W int8 [N,K];
+ * 4: W packed [N,K/2] (low nibble = even k).  K % 64 == 0. */
+int32_t qtx_linear_i8(const int8_t* A, const float* sa, const void* W, const float* sw,
+                      const float* bias, int32_t M, int32_t N, int32_t K, int32_t weight_bits,
+                      int32_t flags, const float* res, float* out, void* stream);
+
+/* Pack int8 values in [-8,7] [N,K] into int4 [N,K/2]. */
+int32_t qtx_pack_int4(const int8_t* q, int32_t N, int32_t K, uint8_t* packed, void* stream);
+
+/* Attention core on quantized Q/K/V laid out [B,S,H*64] with per-token scales [B,S]:
+ * ctx [B,Sq,H*64] fp32.  mask uint8 [B,Sq,Sk] with strides (m_bs, m_is) in elements
+ * (m_is = 0 broadcasts one row, e.g. the encoder's [B,1,S] mask); NULL = keep all. */
+int32_t qtx_attention_i8(const int8_t* q, const float* sq, const int8_t* k, const float* sk,
+                         const int8_t* v, const float* sv, const uint8_t* mask, int64_t m_bs,
+                         int64_t m_is, int32_t B, int32_t H, int32_t Sq, int32_t Sk,
+                         float* ctx, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QTX_H_ */

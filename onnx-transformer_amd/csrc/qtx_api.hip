@@ -1,0 +1,714 @@
+// qtx_api.hip — the C-ABI (include/qtx.h): model handle, per-op entry points and the
+// encoder / decoder / greedy-decode drivers built from the kernels of qtx_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/qtx.h"
+#include "qtx_kernels.h"
+
+using namespace qtx;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(QTX_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                  __LINE__);                                                            \
+  } while (0)
+
+inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+// bump allocator over a caller-provided (or model-owned) device region
+struct Arena {
+  uint8_t* base = nullptr;
+  size_t cap = 0, used = 0;
+  template <class T>
+  T* take(size_t n) {
+    const size_t off = align_up(used);
+    used = off + n * sizeof(T);
+    return base ? reinterpret_cast<T*>(base + off) : nullptr;
+  }
+};
+
+}  // namespace
+
+// One quantized linear: int8 q [N,K] (or packed int4 [N,K/2]), per-channel scale, bias.
+struct QLin {
+  int8_t* q = nullptr;
+  float* s = nullptr;
+  float* b = nullptr;
+  int N = 0, K = 0;
+};
+
+struct EncLayer {
+  QLin qkv, o, w1, w2;
+  const float* ln[2][2];
+};
+struct DecLayer {
+  QLin qkv, o, cq, ckv, co, w1, w2;
+  const float* ln[3][2];
+};
+
+struct qtx_model {
+  qtx_config cfg;
+  std::vector<EncLayer> enc;
+  std::vector<DecLayer> dec;
+  const float* enc_norm[2];
+  const float* dec_norm[2];
+  const float *src_lut, *tgt_lut, *pe, *gen_w, *gen_b;
+  void* mem = nullptr;
+  size_t bytes = 0;
+};
+
+namespace {
+
+// ---- model layout ---------------------------------------------------------------------
+// Linear order per layer follows qtx/weights.py:linear_names():
+//   enc: self_attn.linears.0..3, w_1, w_2        (6 linears, 12 tensors)
+//   dec: self_attn.linears.0..3, src_attn.linears.0..3, w_1, w_2   (10 linears)
+int enc_tensor_base(const qtx_config& c, int L) { return 12 * L; }
+int dec_tensor_base(const qtx_config& c, int L) { return 12 * c.n_layers + 20 * L; }
+int norm_tensor_base(const qtx_config& c) { return 32 * c.n_layers; }
+
+int check_cfg(const qtx_config* c) {
+  if (!c) return fail(QTX_E_INVALID, "null config");
+  if (c->d_model != 512 || c->n_heads * 64 != c->d_model)
+    return fail(QTX_E_UNSUPPORTED, "d_model must be 512 with 64-wide heads");
+  if (c->d_ff % 256 || c->d_ff > 2048 || c->d_ff < 256)
+    return fail(QTX_E_UNSUPPORTED, "d_ff must be a multiple of 256 <= 2048");
+  if (c->weight_bits != 8 && c->weight_bits != 4)
+    return fail(QTX_E_UNSUPPORTED, "weight_bits must be 8 or 4");
+  if (c->n_layers <= 0 || c->src_vocab <= 0 || c->tgt_vocab <= 0 || c->max_len <= 0)
+    return fail(QTX_E_INVALID, "bad config");
+  return QTX_OK;
+}
+
+size_t wbytes(const qtx_config& c, int N, int K) {
+  return c.weight_bits == 8 ? (size_t)N * K : (size_t)N * K / 2;
+}
+
+// quantize rows [row0, row0+N) of lin from fp32 W [N,K] on device
+int quantize_into(const qtx_config& c, QLin& L, int row0, const float* W, const float* b,
+                  int N, int K, int8_t* tmp, hipStream_t st) {
+  RowArgs a{};
+  a.x = W; a.ldx = K; a.rows = N; a.D = K;
+  a.qmax = c.weight_bits == 8 ? 127.0f : 7.0f;
+  a.rpb = N; a.dst_bstride = 0; a.dst_off = 0;
+  a.s = L.s + row0;
+  if (c.weight_bits == 8) {
+    a.q = L.q + (size_t)row0 * K; a.ldq = K;
+    HIPCHK(launch_rows(a, st));
+  } else {
+    a.q = tmp; a.ldq = K;
+    HIPCHK(launch_rows(a, st));
+    HIPCHK(launch_pack_int4(tmp, N, K, reinterpret_cast<uint8_t*>(L.q) + (size_t)row0 * K / 2,
+                            st));
+  }
+  HIPCHK(hipMemcpyAsync(L.b + row0, b, N * sizeof(float), hipMemcpyDeviceToDevice, st));
+  return QTX_OK;
+}
+
+}  // namespace
+
+// =======================================================================================
+extern "C" {
+
+const char* qtx_last_error(void) { return g_err.c_str(); }
+const char* qtx_version(void) { return "qtx 0.1 gfx950"; }
+
+int32_t qtx_model_tensor_count(const qtx_config* cfg) {
+  if (check_cfg(cfg)) return -1;
+  const int L = cfg->n_layers;
+  return 12 * L + 20 * L + 2 * (2 * L + 1 + 3 * L + 1) + 4;
+}
+
+int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n,
+                         const float* pe, void* stream, qtx_model** out) {
+  if (int e = check_cfg(cfg)) return e;
+  if (!t || !pe || !out) return fail(QTX_E_INVALID, "null argument");
+  if (n != qtx_model_tensor_count(cfg))
+    return fail(QTX_E_INVALID, "expected %d tensors, got %d", qtx_model_tensor_count(cfg), n);
+  for (int i = 0; i < n; ++i)
+    if (!t[i]) return fail(QTX_E_INVALID, "tensor %d is null", i);
+  hipStream_t st = (hipStream_t)stream;
+  const qtx_config c = *cfg;
+  const int D = c.d_model, F = c.d_ff, NL = c.n_layers;
+
+  // ---- size the arena (two passes of the same carve) ----
+  auto carve = [&](qtx_model* m, Arena& ar) {
+    auto lin = [&](QLin& L, int N, int K) {
+      L.N = N; L.K = K;
+      L.q = ar.take<int8_t>(wbytes(c, N, K));
+      L.s = ar.take<float>(N);
+      L.b = ar.take<float>(N);
+    };
+    m->enc.resize(NL);
+    m->dec.resize(NL);
+    for (auto& e : m->enc) { lin(e.qkv, 3 * D, D); lin(e.o, D, D); lin(e.w1, F, D); lin(e.w2, D, F); }
+    for (auto& d : m->dec) {
+      lin(d.qkv, 3 * D, D); lin(d.o, D, D); lin(d.cq, D, D); lin(d.ckv, 2 * D, D);
+      lin(d.co, D, D); lin(d.w1, F, D); lin(d.w2, D, F);
+    }
+    float* norms = ar.take<float>((size_t)2 * D * (5 * NL + 2));
+    float* src_lut = ar.take<float>((size_t)c.src_vocab * D);
+    float* tgt_lut = ar.take<float>((size_t)c.tgt_vocab * D);
+    float* pe_d = ar.take<float>((size_t)c.max_len * D);
+    float* gw = ar.take<float>((size_t)c.tgt_vocab * D);
+    float* gb = ar.take<float>(c.tgt_vocab);
+    int8_t* tmp = ar.take<int8_t>((size_t)F * D);
+    return std::make_tuple(norms, src_lut, tgt_lut, pe_d, gw, gb, tmp);
+  };
+  qtx_model* m = new qtx_model();
+  m->cfg = c;
+  Arena sizing;
+  carve(m, sizing);
+  const size_t bytes = align_up(sizing.used);
+  void* mem = nullptr;
+  hipError_t he = hipMalloc(&mem, bytes);
+  if (he != hipSuccess) {
+    delete m;
+    return fail(QTX_E_HIP, "hipMalloc(%zu): %s", bytes, hipGetErrorString(he));
+  }
+  m->mem = mem;
+  m->bytes = bytes;
+  Arena ar;
+  ar.base = (uint8_t*)mem;
+  ar.cap = bytes;
+  float *norms, *src_lut, *tgt_lut, *pe_d, *gw, *gb;
+  int8_t* tmp;
+  std::tie(norms, src_lut, tgt_lut, pe_d, gw, gb, tmp) = carve(m, ar);
+
+  int rc = QTX_OK;
+  auto Q = [&](QLin& L, int row0, int ti, int N, int K) {
+    if (rc == QTX_OK) rc = quantize_into(c, L, row0, t[ti], t[ti + 1], N, K, tmp, st);
+  };
+  for (int l = 0; l < NL; ++l) {
+    const int b = enc_tensor_base(c, l);
+    EncLayer& e = m->enc[l];
+    for (int i = 0; i < 3; ++i) Q(e.qkv, i * D, b + 2 * i, D, D);
+    Q(e.o, 0, b + 6, D, D);
+    Q(e.w1, 0, b + 8, F, D);
+    Q(e.w2, 0, b + 10, D, F);
+  }
+  for (int l = 0; l < NL; ++l) {
+    const int b = dec_tensor_base(c, l);
+    DecLayer& d = m->dec[l];
+    for (int i = 0; i < 3; ++i) Q(d.qkv, i * D, b + 2 * i, D, D);
+    Q(d.o, 0, b + 6, D, D);
+    Q(d.cq, 0, b + 8, D, D);
+    Q(d.ckv, 0, b + 10, D, D);
+    Q(d.ckv, D, b + 12, D, D);
+    Q(d.co, 0, b + 14, D, D);
+    Q(d.w1, 0, b + 16, F, D);
+    Q(d.w2, 0, b + 18, D, F);
+  }
+  if (rc) { qtx_model_destroy(m); return rc; }
+  // norms: order of weights.py:norm_names — enc L x 2, enc final, dec L x 3, dec final
+  const int nb = norm_tensor_base(c);
+  const int n_norms = 5 * NL + 2;
+  for (int i = 0; i < n_norms; ++i)
+    for (int j = 0; j < 2; ++j) {
+      he = hipMemcpyAsync(norms + (size_t)(2 * i + j) * D, t[nb + 2 * i + j], D * sizeof(float),
+                          hipMemcpyDeviceToDevice, st);
+      if (he != hipSuccess) { qtx_model_destroy(m); return fail(QTX_E_HIP, "copy norms"); }
+    }
+  auto nrm = [&](int i, int j) -> const float* { return norms + (size_t)(2 * i + j) * D; };
+  int ni = 0;
+  for (int l = 0; l < NL; ++l)
+    for (int s = 0; s < 2; ++s, ++ni) { m->enc[l].ln[s][0] = nrm(ni, 0); m->enc[l].ln[s][1] = nrm(ni, 1); }
+  m->enc_norm[0] = nrm(ni, 0); m->enc_norm[1] = nrm(ni, 1); ++ni;
+  for (int l = 0; l < NL; ++l)
+    for (int s = 0; s < 3; ++s, ++ni) { m->dec[l].ln[s][0] = nrm(ni, 0); m->dec[l].ln[s][1] = nrm(ni, 1); }
+  m->dec_norm[0] = nrm(ni, 0); m->dec_norm[1] = nrm(ni, 1); ++ni;
+  const int eb = nb + 2 * n_norms;
+  struct Cp { float* dst; const float* src; size_t n; } cps[] = {
+      {src_lut, t[eb], (size_t)c.src_vocab * D}, {tgt_lut, t[eb + 1], (size_t)c.tgt_vocab * D},
+      {gw, t[eb + 2], (size_t)c.tgt_vocab * D}, {gb, t[eb + 3], (size_t)c.tgt_vocab},
+      {pe_d, pe, (size_t)c.max_len * D}};
+  for (auto& cp : cps) {
+    he = hipMemcpyAsync(cp.dst, cp.src, cp.n * sizeof(float), hipMemcpyDeviceToDevice, st);
+    if (he != hipSuccess) { qtx_model_destroy(m); return fail(QTX_E_HIP, "copy tables"); }
+  }
+  m->src_lut = src_lut; m->tgt_lut = tgt_lut; m->pe = pe_d; m->gen_w = gw; m->gen_b = gb;
+  he = hipStreamSynchronize(st);
+  if (he != hipSuccess) {
+    qtx_model_destroy(m);
+    return fail(QTX_E_HIP, "model create: %s", hipGetErrorString(he));
+  }
+  *out = m;
+  return QTX_OK;
+}
+
+int32_t qtx_model_destroy(qtx_model* m) {
+  if (!m) return QTX_OK;
+  if (m->mem) (void)hipFree(m->mem);
+  delete m;
+  return QTX_OK;
+}
+
+size_t qtx_model_device_bytes(const qtx_model* m) { return m ? m->bytes : 0; }
+
+}  // extern "C"
+
+// =======================================================================================
+// drivers
+// =======================================================================================
+namespace {
+
+// scratch for one stack pass over M rows (fp32 residual stream + quant buffers)
+struct Scratch {
+  float* x;      // [M, D] residual stream
+  int8_t* a8;    // [M, F] activation ints (max K)
+  float* sa;     // [M]
+  float* y;      // [M, max(3D, F)] GEMM output
+  int8_t* q8;    // [M, D]
+  float* sq;     // [M]
+  int8_t* k8;    // [M, D]
+  float* sk;
+  int8_t* v8;    // [M, D]
+  float* sv;
+  float* ctx;    // [M, D]
+};
+
+Scratch carve_scratch(Arena& ar, const qtx_config& c, long M) {
+  const int D = c.d_model, F = c.d_ff;
+  const int Y = 3 * D > F ? 3 * D : F;
+  Scratch s;
+  s.x = ar.take<float>(M * D);
+  s.a8 = ar.take<int8_t>(M * F);
+  s.sa = ar.take<float>(M);
+  s.y = ar.take<float>(M * Y);
+  s.q8 = ar.take<int8_t>(M * D); s.sq = ar.take<float>(M);
+  s.k8 = ar.take<int8_t>(M * D); s.sk = ar.take<float>(M);
+  s.v8 = ar.take<int8_t>(M * D); s.sv = ar.take<float>(M);
+  s.ctx = ar.take<float>(M * D);
+  return s;
+}
+
+// ---- building blocks ------------------------------------------------------------------
+RowArgs rows_quant(const float* x, long ldx, int rows, int D, int8_t* q, float* s) {
+  RowArgs a{};
+  a.x = x; a.ldx = ldx; a.rows = rows; a.D = D;
+  a.q = q; a.ldq = D; a.s = s; a.qmax = 127.0f;
+  a.rpb = rows > 0 ? rows : 1; a.dst_bstride = 0; a.dst_off = 0;
+  return a;
+}
+
+int ln_quant(const float* x, int rows, const float* const* ln, int D, int8_t* q, float* s,
+             hipStream_t st) {
+  RowArgs a = rows_quant(x, D, rows, D, q, s);
+  a.ln_a = ln[0]; a.ln_b = ln[1];
+  HIPCHK(launch_rows(a, st));
+  return QTX_OK;
+}
+
+int ln_out(const float* x, int rows, const float* const* ln, int D, float* y, hipStream_t st) {
+  RowArgs a{};
+  a.x = x; a.ldx = D; a.rows = rows; a.D = D; a.ln_a = ln[0]; a.ln_b = ln[1];
+  a.yout = y; a.ldy = D; a.rpb = rows > 0 ? rows : 1;
+  HIPCHK(launch_rows(a, st));
+  return QTX_OK;
+}
+
+int quant(const float* x, long ldx, int rows, int D, int8_t* q, float* s, hipStream_t st) {
+  HIPCHK(launch_rows(rows_quant(x, ldx, rows, D, q, s), st));
+  return QTX_OK;
+}
+
+int linear(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa, int M,
+           int flags, const float* res, float* out, long ldo, hipStream_t st) {
+  GemmArgs g{};
+  g.A = a8; g.lda = L.K; g.sa = sa;
+  g.W = L.q; g.ldw = c.weight_bits == 8 ? L.K : L.K / 2; g.sw = L.s; g.bias = L.b;
+  g.out = out; g.ldo = ldo; g.res = res; g.ldr = ldo;
+  g.M = M; g.N = L.N; g.K = L.K; g.flags = flags;
+  HIPCHK(launch_gemm(g, c.weight_bits, st));
+  return QTX_OK;
+}
+
+AttnArgs attn_args(const Scratch& s, int B, int Sq, int Sk, long kbs_rows) {
+  AttnArgs a{};
+  const int D = 512;
+  a.q = s.q8; a.q_bs = (long)Sq * D; a.q_ld = D; a.sq = s.sq; a.sq_bs = Sq;
+  a.k = s.k8; a.k_bs = kbs_rows * D; a.k_ld = D; a.sk = s.sk; a.sk_bs = kbs_rows;
+  a.v = s.v8; a.v_bs = kbs_rows * D; a.v_ld = D; a.sv = s.sv; a.sv_bs = kbs_rows;
+  a.ctx = s.ctx; a.c_bs = (long)Sq * D; a.c_ld = D;
+  a.B = B; a.H = 8; a.Sq = Sq; a.Sk = Sk;
+  return a;
+}
+
+#define RC(expr)                       \
+  do {                                 \
+    int rc_ = (expr);                  \
+    if (rc_ != QTX_OK) return rc_;     \
+  } while (0)
+
+// Self-attention sublayer: x += O(attn(LN(x)))   (sublayer_connection.py:15-17,
+// attention.py:39-67).  Q/K/V come out of ONE N=3D GEMM and are quantized per token.
+int self_attn_block(const qtx_config& c, const QLin& qkv, const QLin& o,
+                    const float* const* ln, Scratch& s, int B, int S, const uint8_t* mask,
+                    long m_bs, long m_is, hipStream_t st) {
+  const int D = c.d_model, M = B * S;
+  RC(ln_quant(s.x, M, ln, D, s.a8, s.sa, st));
+  RC(linear(c, qkv, s.a8, s.sa, M, 0, nullptr, s.y, 3 * D, st));
+  RC(quant(s.y, 3 * D, M, D, s.q8, s.sq, st));
+  RC(quant(s.y + D, 3 * D, M, D, s.k8, s.sk, st));
+  RC(quant(s.y + 2 * D, 3 * D, M, D, s.v8, s.sv, st));
+  AttnArgs a = attn_args(s, B, S, S, S);
+  a.mask = mask; a.m_bs = m_bs; a.m_is = m_is;
+  HIPCHK(launch_attention(a, st));
+  RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+  RC(linear(c, o, s.a8, s.sa, M, EPI_RESIDUAL, s.x, s.x, D, st));
+  return QTX_OK;
+}
+
+// FFN sublayer: x += w_2(relu(w_1(LN(x))))   (position_feed_forward.py:11-12)
+int ffn_block(const qtx_config& c, const QLin& w1, const QLin& w2, const float* const* ln,
+              Scratch& s, int M, hipStream_t st) {
+  const int D = c.d_model, F = c.d_ff;
+  RC(ln_quant(s.x, M, ln, D, s.a8, s.sa, st));
+  RC(linear(c, w1, s.a8, s.sa, M, EPI_RELU, nullptr, s.y, F, st));
+  RC(quant(s.y, F, M, F, s.a8, s.sa, st));
+  RC(linear(c, w2, s.a8, s.sa, M, EPI_RESIDUAL, s.x, s.x, D, st));
+  return QTX_OK;
+}
+
+int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, int S,
+                float* out, Scratch& s, hipStream_t st) {
+  const qtx_config& c = m->cfg;
+  const int D = c.d_model, M = B * S;
+  if (x != s.x) HIPCHK(hipMemcpyAsync(s.x, x, (size_t)M * D * 4, hipMemcpyDeviceToDevice, st));
+  for (const EncLayer& L : m->enc) {
+    RC(self_attn_block(c, L.qkv, L.o, L.ln[0], s, B, S, mask, S, 0, st));
+    RC(ffn_block(c, L.w1, L.w2, L.ln[1], s, M, st));
+  }
+  RC(ln_out(s.x, M, m->enc_norm, D, out, st));
+  return QTX_OK;
+}
+
+size_t enc_ws(const qtx_config& c, int B, int S) {
+  Arena ar;
+  carve_scratch(ar, c, (long)B * S);
+  return align_up(ar.used);
+}
+
+// decoder-specific scratch: quantized memory + cross K/V for all layers
+struct CrossKV {
+  int8_t* am8;  // [B*S, D] quantized memory (per token, layer independent)
+  float* sam;
+  std::vector<int8_t*> k8, v8;
+  std::vector<float*> sk, sv;
+  float* y;     // [B*S, 2D]
+};
+
+CrossKV carve_cross(Arena& ar, const qtx_config& c, long Ms) {
+  const int D = c.d_model;
+  CrossKV x;
+  x.am8 = ar.take<int8_t>(Ms * D);
+  x.sam = ar.take<float>(Ms);
+  x.y = ar.take<float>(Ms * 2 * D);
+  for (int l = 0; l < c.n_layers; ++l) {
+    x.k8.push_back(ar.take<int8_t>(Ms * D)); x.sk.push_back(ar.take<float>(Ms));
+    x.v8.push_back(ar.take<int8_t>(Ms * D)); x.sv.push_back(ar.take<float>(Ms));
+  }
+  return x;
+}
+
+// memory -> per-layer cross K/V (get_quantized_model.py:160-168: K/V outputs quantized)
+int cross_kv(const qtx_model* m, const float* memory, int Ms, CrossKV& x, hipStream_t st) {
+  const qtx_config& c = m->cfg;
+  const int D = c.d_model;
+  RC(quant(memory, D, Ms, D, x.am8, x.sam, st));
+  for (int l = 0; l < c.n_layers; ++l) {
+    RC(linear(c, m->dec[l].ckv, x.am8, x.sam, Ms, 0, nullptr, x.y, 2 * D, st));
+    RC(quant(x.y, 2 * D, Ms, D, x.k8[l], x.sk[l], st));
+    RC(quant(x.y + D, 2 * D, Ms, D, x.v8[l], x.sv[l], st));
+  }
+  return QTX_OK;
+}
+
+// Cross-attention sublayer: x += O(attn(LN(x) -> Q, memory -> K/V)), decoder.py:32
+int cross_attn_block(const qtx_model* m, const DecLayer& L, int l, Scratch& s,
+                     const CrossKV& x, int B, int T, int S, const uint8_t* src_mask,
+                     hipStream_t st) {
+  const qtx_config& c = m->cfg;
+  const int D = c.d_model, M = B * T;
+  RC(ln_quant(s.x, M, L.ln[1], D, s.a8, s.sa, st));
+  RC(linear(c, L.cq, s.a8, s.sa, M, 0, nullptr, s.y, D, st));
+  RC(quant(s.y, D, M, D, s.q8, s.sq, st));
+  AttnArgs a = attn_args(s, B, T, S, S);
+  a.k = x.k8[l]; a.sk = x.sk[l]; a.v = x.v8[l]; a.sv = x.sv[l];
+  a.mask = src_mask; a.m_bs = S; a.m_is = 0;
+  HIPCHK(launch_attention(a, st));
+  RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+  RC(linear(c, L.co, s.a8, s.sa, M, EPI_RESIDUAL, s.x, s.x, D, st));
+  return QTX_OK;
+}
+
+size_t dec_ws(const qtx_config& c, int B, int T, int S) {
+  Arena ar;
+  carve_scratch(ar, c, (long)B * T);
+  carve_cross(ar, c, (long)B * S);
+  return align_up(ar.used);
+}
+
+// greedy decode workspace: encoder scratch, decoder step scratch (M=B), cross K/V,
+// self K/V caches [L][B][max_len][D], memory, logits, step counter
+struct GreedyWS {
+  Scratch enc, dec;
+  CrossKV cross;
+  std::vector<int8_t*> kc, vc;
+  std::vector<float*> skc, svc;
+  float* memory;
+  float* xo;
+  float* logits;
+  int* step;
+};
+
+GreedyWS carve_greedy(Arena& ar, const qtx_config& c, int B, int S, int max_len) {
+  GreedyWS g;
+  const int D = c.d_model;
+  g.enc = carve_scratch(ar, c, (long)B * S);
+  g.dec = carve_scratch(ar, c, B);
+  g.cross = carve_cross(ar, c, (long)B * S);
+  for (int l = 0; l < c.n_layers; ++l) {
+    g.kc.push_back(ar.take<int8_t>((size_t)B * max_len * D));
+    g.skc.push_back(ar.take<float>((size_t)B * max_len));
+    g.vc.push_back(ar.take<int8_t>((size_t)B * max_len * D));
+    g.svc.push_back(ar.take<float>((size_t)B * max_len));
+  }
+  g.memory = ar.take<float>((size_t)B * S * D);
+  g.xo = ar.take<float>((size_t)B * D);
+  g.logits = ar.take<float>((size_t)B * c.tgt_vocab);
+  g.step = ar.take<int>(4);
+  return g;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t qtx_encoder_workspace_size(const qtx_model* m, int32_t B, int32_t S) {
+  return m ? enc_ws(m->cfg, B, S) : 0;
+}
+size_t qtx_decoder_workspace_size(const qtx_model* m, int32_t B, int32_t T, int32_t S) {
+  return m ? dec_ws(m->cfg, B, T, S) : 0;
+}
+size_t qtx_greedy_workspace_size(const qtx_model* m, int32_t B, int32_t S, int32_t max_len) {
+  if (!m) return 0;
+  Arena ar;
+  carve_greedy(ar, m->cfg, B, S, max_len);
+  return align_up(ar.used);
+}
+
+int32_t qtx_encoder_forward(const qtx_model* m, const float* x, const uint8_t* src_mask,
+                            int32_t B, int32_t S, float* out, void* ws, size_t ws_bytes,
+                            void* stream) {
+  if (!m || !x || !src_mask || !out || !ws) return fail(QTX_E_INVALID, "null argument");
+  if (B <= 0 || S <= 0 || S > 512) return fail(QTX_E_INVALID, "bad shape B=%d S=%d", B, S);
+  if (ws_bytes < enc_ws(m->cfg, B, S)) return fail(QTX_E_WORKSPACE, "workspace too small");
+  Arena ar;
+  ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
+  Scratch s = carve_scratch(ar, m->cfg, (long)B * S);
+  return encoder_run(m, x, src_mask, B, S, out, s, (hipStream_t)stream);
+}
+
+int32_t qtx_decoder_forward(const qtx_model* m, const float* y, const float* memory,
+                            const uint8_t* src_mask, const uint8_t* tgt_mask,
+                            int32_t tgt_mask_batched, int32_t B, int32_t T, int32_t S,
+                            float* out, void* ws, size_t ws_bytes, void* stream) {
+  if (!m || !y || !memory || !src_mask || !tgt_mask || !out || !ws)
+    return fail(QTX_E_INVALID, "null argument");
+  if (B <= 0 || T <= 0 || S <= 0 || T > 512 || S > 512)
+    return fail(QTX_E_INVALID, "bad shape B=%d T=%d S=%d", B, T, S);
+  if (ws_bytes < dec_ws(m->cfg, B, T, S)) return fail(QTX_E_WORKSPACE, "workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const qtx_config& c = m->cfg;
+  const int D = c.d_model, M = B * T;
+  Arena ar;
+  ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
+  Scratch s = carve_scratch(ar, c, M);
+  CrossKV x = carve_cross(ar, c, (long)B * S);
+  RC(cross_kv(m, memory, B * S, x, st));
+  HIPCHK(hipMemcpyAsync(s.x, y, (size_t)M * D * 4, hipMemcpyDeviceToDevice, st));
+  for (int l = 0; l < c.n_layers; ++l) {
+    const DecLayer& L = m->dec[l];
+    RC(self_attn_block(c, L.qkv, L.o, L.ln[0], s, B, T, tgt_mask,
+                       tgt_mask_batched ? (long)T * T : 0, T, st));
+    RC(cross_attn_block(m, L, l, s, x, B, T, S, src_mask, st));
+    RC(ffn_block(c, L.w1, L.w2, L.ln[2], s, M, st));
+  }
+  RC(ln_out(s.x, M, m->dec_norm, D, out, st));
+  return QTX_OK;
+}
+
+int32_t qtx_embed(const qtx_model* m, int32_t which, const int64_t* ids, int32_t B, int32_t T,
+                  int32_t pos0, float* out, void* stream) {
+  if (!m || !ids || !out) return fail(QTX_E_INVALID, "null argument");
+  if (pos0 < 0 || pos0 + T > m->cfg.max_len)
+    return fail(QTX_E_INVALID, "positions exceed max_len %d", m->cfg.max_len);
+  const float* lut = which ? m->tgt_lut : m->src_lut;
+  const int vocab = which ? m->cfg.tgt_vocab : m->cfg.src_vocab;
+  HIPCHK(launch_embed(ids, T, B, T, nullptr, pos0, lut, vocab, m->pe, m->cfg.max_len, out,
+                      (long)T * m->cfg.d_model, (hipStream_t)stream));
+  return QTX_OK;
+}
+
+int32_t qtx_generator(const qtx_model* m, const float* x, int32_t M, float* logp,
+                      int64_t* ids, void* ws, size_t ws_bytes, void* stream) {
+  if (!m || !x || !ws) return fail(QTX_E_INVALID, "null argument");
+  const int V = m->cfg.tgt_vocab;
+  if (ws_bytes < (size_t)M * V * sizeof(float)) return fail(QTX_E_WORKSPACE, "ws too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* logits = (float*)ws;
+  HIPCHK(launch_generator(x, m->cfg.d_model, M, m->gen_w, m->gen_b, V, logits, st));
+  HIPCHK(launch_logsoftmax_argmax(logits, M, V, logp, ids, 1, nullptr, 0, st));
+  return QTX_OK;
+}
+
+int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t* src_mask,
+                          int32_t B, int32_t S, int32_t max_len, int64_t start, int64_t* ids,
+                          void* ws, size_t ws_bytes, void* stream) {
+  if (!m || !src || !src_mask || !ids || !ws) return fail(QTX_E_INVALID, "null argument");
+  const qtx_config& c = m->cfg;
+  if (B <= 0 || S <= 0 || S > 512 || max_len < 1 || max_len > 512 || max_len > c.max_len ||
+      S > c.max_len)
+    return fail(QTX_E_INVALID, "bad shape B=%d S=%d max_len=%d", B, S, max_len);
+  if (ws_bytes < qtx_greedy_workspace_size(m, B, S, max_len))
+    return fail(QTX_E_WORKSPACE, "workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int D = c.d_model;
+  Arena ar;
+  ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
+  GreedyWS g = carve_greedy(ar, c, B, S, max_len);
+
+  // encoder: memory = encode(src_embed(src), src_mask)
+  HIPCHK(launch_embed(src, S, B, S, nullptr, 0, m->src_lut, c.src_vocab, m->pe, c.max_len,
+                      g.enc.x, (long)S * D, st));
+  RC(encoder_run(m, g.enc.x, src_mask, B, S, g.memory, g.enc, st));
+  RC(cross_kv(m, g.memory, B * S, g.cross, st));
+
+  // ids[:, 0] = start ; step counter = 0
+  HIPCHK(launch_fill_col(ids, max_len, B, start, st));
+  HIPCHK(hipMemsetAsync(g.step, 0, 16, st));
+  Scratch& s = g.dec;
+  for (int t = 0; t + 1 < max_len; ++t) {
+    // x = tgt_embed(ys[:, step]) at position step
+    HIPCHK(launch_embed(ids, max_len, B, 1, g.step, 0, m->tgt_lut, c.tgt_vocab, m->pe,
+                        c.max_len, s.x, D, st));
+    for (int l = 0; l < c.n_layers; ++l) {
+      const DecLayer& L = m->dec[l];
+      // masked self-attention with KV cache
+      RC(ln_quant(s.x, B, L.ln[0], D, s.a8, s.sa, st));
+      RC(linear(c, L.qkv, s.a8, s.sa, B, 0, nullptr, s.y, 3 * D, st));
+      RC(quant(s.y, 3 * D, B, D, s.q8, s.sq, st));
+      RowArgs kr = rows_quant(s.y + D, 3 * D, B, D, g.kc[l], g.skc[l]);
+      kr.rpb = 1; kr.dst_bstride = max_len; kr.dst_off_dev = g.step;
+      HIPCHK(launch_rows(kr, st));
+      RowArgs vr = rows_quant(s.y + 2 * D, 3 * D, B, D, g.vc[l], g.svc[l]);
+      vr.rpb = 1; vr.dst_bstride = max_len; vr.dst_off_dev = g.step;
+      HIPCHK(launch_rows(vr, st));
+      AttnArgs a = attn_args(s, B, 1, 0, max_len);
+      a.k = g.kc[l]; a.sk = g.skc[l]; a.v = g.vc[l]; a.sv = g.svc[l];
+      a.sk_dev = g.step; a.sk_add = 1;
+      HIPCHK(launch_attention(a, st));
+      RC(quant(s.ctx, D, B, D, s.a8, s.sa, st));
+      RC(linear(c, L.o, s.a8, s.sa, B, EPI_RESIDUAL, s.x, s.x, D, st));
+      RC(cross_attn_block(m, L, l, s, g.cross, B, 1, S, src_mask, st));
+      RC(ffn_block(c, L.w1, L.w2, L.ln[2], s, B, st));
+    }
+    RC(ln_out(s.x, B, m->dec_norm, D, g.xo, st));
+    HIPCHK(launch_generator(g.xo, D, B, m->gen_w, m->gen_b, c.tgt_vocab, g.logits, st));
+    HIPCHK(launch_logsoftmax_argmax(g.logits, B, c.tgt_vocab, nullptr, ids, max_len, g.step, 1,
+                                    st));
+    HIPCHK(launch_step_inc(g.step, st));
+  }
+  return QTX_OK;
+}
+
+// ---- per-op entry points ---------------------------------------------------------------
+int32_t qtx_row_quant(const float* x, int32_t rows, int32_t D, float qmax, int8_t* q,
+                      float* s, void* stream) {
+  if (!x || !q || !s) return fail(QTX_E_INVALID, "null argument");
+  RowArgs a = rows_quant(x, D, rows, D, q, s);
+  a.qmax = qmax;
+  hipError_t e = launch_rows(a, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "D=%d unsupported", D);
+  HIPCHK(e);
+  return QTX_OK;
+}
+
+int32_t qtx_layernorm_quant(const float* x, const float* a, const float* b, int32_t rows,
+                            int32_t D, float* y, int8_t* q, float* s, void* stream) {
+  if (!x || !a || !b || (!y && !q)) return fail(QTX_E_INVALID, "null argument");
+  RowArgs r{};
+  r.x = x; r.ldx = D; r.rows = rows; r.D = D; r.ln_a = a; r.ln_b = b;
+  r.yout = y; r.ldy = D; r.q = q; r.ldq = D; r.s = s; r.qmax = 127.0f;
+  r.rpb = rows > 0 ? rows : 1;
+  hipError_t e = launch_rows(r, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "D=%d unsupported", D);
+  HIPCHK(e);
+  return QTX_OK;
+}
+
+int32_t qtx_linear_i8(const int8_t* A, const float* sa, const void* W, const float* sw,
+                      const float* bias, int32_t M, int32_t N, int32_t K, int32_t weight_bits,
+                      int32_t flags, const float* res, float* out, void* stream) {
+  if (!A || !sa || !W || !sw || !bias || !out) return fail(QTX_E_INVALID, "null argument");
+  if ((flags & EPI_RESIDUAL) && !res) return fail(QTX_E_INVALID, "residual flag without res");
+  if (K % 64) return fail(QTX_E_UNSUPPORTED, "K=%d not a multiple of 64", K);
+  GemmArgs g{};
+  g.A = A; g.lda = K; g.sa = sa; g.W = (const int8_t*)W;
+  g.ldw = weight_bits == 8 ? K : K / 2; g.sw = sw; g.bias = bias;
+  g.out = out; g.ldo = N; g.res = res; g.ldr = N;
+  g.M = M; g.N = N; g.K = K; g.flags = flags;
+  hipError_t e = launch_gemm(g, weight_bits, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "weight_bits=%d", weight_bits);
+  HIPCHK(e);
+  return QTX_OK;
+}
+
+int32_t qtx_pack_int4(const int8_t* q, int32_t N, int32_t K, uint8_t* packed, void* stream) {
+  if (!q || !packed || K % 2) return fail(QTX_E_INVALID, "bad argument");
+  HIPCHK(launch_pack_int4(q, N, K, packed, (hipStream_t)stream));
+  return QTX_OK;
+}
+
+int32_t qtx_attention_i8(const int8_t* q, const float* sq, const int8_t* k, const float* sk,
+                         const int8_t* v, const float* sv, const uint8_t* mask, int64_t m_bs,
+                         int64_t m_is, int32_t B, int32_t H, int32_t Sq, int32_t Sk,
+                         float* ctx, void* stream) {
+  if (!q || !sq || !k || !sk || !v || !sv || !ctx) return fail(QTX_E_INVALID, "null argument");
+  if (Sk <= 0 || Sk > 512 || Sq <= 0) return fail(QTX_E_UNSUPPORTED, "Sk=%d (max 512)", Sk);
+  const long D = (long)H * 64;
+  AttnArgs a{};
+  a.q = q; a.q_bs = Sq * D; a.q_ld = D; a.sq = sq; a.sq_bs = Sq;
+  a.k = k; a.k_bs = Sk * D; a.k_ld = D; a.sk = sk; a.sk_bs = Sk;
+  a.v = v; a.v_bs = Sk * D; a.v_ld = D; a.sv = sv; a.sv_bs = Sk;
+  a.mask = mask; a.m_bs = m_bs; a.m_is = m_is;
+  a.ctx = ctx; a.c_bs = Sq * D; a.c_ld = D;
+  a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
+  HIPCHK(launch_attention(a, (hipStream_t)stream));
+  return QTX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,87 @@
+"""ctypes binding of libqtx.so (include/qtx.h).
+
+Loading fails loudly: there is no CPU fallback in the product path.  torch is used only
+for device memory and the current HIP stream (plumbing, not compute).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+from . import _build
+
+_lib = None
+
+
+class QtxError(RuntimeError):
+    """Raised for a non-zero qtx_status (the reference raises on bad feeds/shapes too)."""
+
+    def __init__(self, fn, code, msg):
+        super().__init__(f"{fn} failed (status {code}): {msg}")
+        self.code = code
+
+
+class QtxConfig(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in
+                ("src_vocab", "tgt_vocab", "n_layers", "d_model", "d_ff", "n_heads",
+                 "max_len", "weight_bits")]
+
+
+P = C.c_void_p
+I32, I64, SZ, F32 = C.c_int32, C.c_int64, C.c_size_t, C.c_float
+
+# name -> (restype, argtypes); must match include/qtx.h
+SIGNATURES = {
+    "qtx_last_error": (C.c_char_p, []),
+    "qtx_version": (C.c_char_p, []),
+    "qtx_model_tensor_count": (I32, [C.POINTER(QtxConfig)]),
+    "qtx_model_create": (I32, [C.POINTER(QtxConfig), C.POINTER(P), I32, P, P, C.POINTER(P)]),
+    "qtx_model_destroy": (I32, [P]),
+    "qtx_model_device_bytes": (SZ, [P]),
+    "qtx_encoder_workspace_size": (SZ, [P, I32, I32]),
+    "qtx_decoder_workspace_size": (SZ, [P, I32, I32, I32]),
+    "qtx_greedy_workspace_size": (SZ, [P, I32, I32, I32]),
+    "qtx_encoder_forward": (I32, [P, P, P, I32, I32, P, P, SZ, P]),
+    "qtx_decoder_forward": (I32, [P, P, P, P, P, I32, I32, I32, I32, P, P, SZ, P]),
+    "qtx_greedy_decode": (I32, [P, P, P, I32, I32, I32, I64, P, P, SZ, P]),
+    "qtx_embed": (I32, [P, I32, P, I32, I32, I32, P, P]),
+    "qtx_generator": (I32, [P, P, I32, P, P, P, SZ, P]),
+    "qtx_row_quant": (I32, [P, I32, I32, F32, P, P, P]),
+    "qtx_layernorm_quant": (I32, [P, P, P, I32, I32, P, P, P, P]),
+    "qtx_linear_i8": (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, P, P, P]),
+    "qtx_pack_int4": (I32, [P, I32, I32, P, P]),
+    "qtx_attention_i8": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, P]),
+}
+
+
+def header_symbols(path=None) -> list[str]:
+    """Function names declared in include/qtx.h (used by the ABI test)."""
+    path = path or os.path.join(_build.REPO, "include", "qtx.h")
+    text = open(path).read()
+    return sorted(set(re.findall(r"\b(qtx_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib(build: bool = True):
+    """Load (building first if sources changed) libqtx.so; raises if impossible."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.build() if build else _build.LIB
+    if not os.path.exists(path):
+        raise RuntimeError(f"libqtx.so missing at {path}; run __graft_entry__.build()")
+    L = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    _lib = L
+    return L
+
+
+def call(name, *args):
+    """Call an int32-status entry point and raise QtxError on failure."""
+    L = lib()
+    rc = getattr(L, name)(*args)
+    if rc != 0:
+        raise QtxError(name, rc, L.qtx_last_error().decode(errors="replace"))
+    return rc

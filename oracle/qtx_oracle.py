@@ -1,0 +1,428 @@
+"""CPU ORACLE — test infrastructure only.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module, and only as the checker / the timed CPU baseline.  The product path
+(``onnx-transformer_amd/qtx``) never imports it.
+
+What it is: a numpy restatement of the reference's W8A8 inference arithmetic
+(gebegebegebe/onnx-transformer).  The reference executes this arithmetic as fake-quant
+fp32 graphs on ONNXRuntime-CPU; here it is restated as exact integer GEMMs
+(int32 accumulators) plus a *canonical fp32 evaluation order* for every float step.
+The canonical order is the contract the HIP kernels implement, so the GPU path and this
+oracle agree bit-for-bit (see DESIGN.md §3 "numerics contract"):
+
+* no FMA contraction except where the canonical order says ``fma`` (PV and generator dots);
+* LayerNorm / softmax / log-softmax sums use a fixed lane-split + xor-butterfly tree;
+* softmax uses :func:`qexp`, a fixed polynomial exp that both sides evaluate identically.
+
+Parity pinning: tests/test_oracle_golden.py checks this oracle against golden vectors
+produced by importing the reference's own PyTorch modules (tests/golden/make_golden.py);
+the ORT CPU path itself is unrunnable here, so ORT-level parity is unpinned.
+
+The fma emulation (:func:`fma32`) computes in float64 and rounds once to float32; it is
+exact except when the float64 rounding lands exactly on a float32 midpoint (probability
+~2^-29 per operation), which is documented in DESIGN.md.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+f32 = np.float32
+EPS_SCALE = f32(1e-5)          # quant_linear.py:11,37 clamp(min=1e-5)
+LN_EPS = f32(1e-6)             # layer_norm.py:6
+MASK_FILL = f32(-1e9)          # attention.py:29
+EXP_FLUSH = f32(-80.0)         # qexp() returns exactly 0 below this (keeps results normal)
+
+
+# ---------------------------------------------------------------------------------------
+# elementary canonical operations
+# ---------------------------------------------------------------------------------------
+
+def fma32(a, b, c):
+    """float32 fused multiply-add, emulated in float64 (see module docstring)."""
+    return (np.asarray(a, np.float64) * np.asarray(b, np.float64)
+            + np.asarray(c, np.float64)).astype(f32)
+
+
+_H = lambda h: f32(float.fromhex(h))    # exact float32 constants, shared with qtx_common.h
+_EXP_C = [_H("0x1.a01a02p-13"), _H("0x1.6c16c2p-10"), _H("0x1.111112p-7"),   # 1/7! .. 1/5!
+          _H("0x1.555556p-5"), _H("0x1.555556p-3"), f32(0.5), f32(1.0), f32(1.0)]
+_LOG2E = _H("0x1.715476p+0")
+_LN2_HI = _H("0x1.62e4p-1")
+_LN2_LO = _H("0x1.7f7d1cp-20")
+
+
+def qexp(x):
+    """Canonical fp32 exp: Cody-Waite reduction + degree-7 Taylor, Horner, no FMA.
+
+    Mirrored exactly by ``qexp`` in onnx-transformer_amd/csrc/qtx_common.h.
+    Inputs below -80 give exactly 0 (the softmax/log-softmax callers only need e^x for
+    x <= 0, where such terms cannot change a 1/127-quantized probability).
+    """
+    x = np.asarray(x, f32)
+    xc = np.maximum(x, f32(-100.0))
+    n = np.rint(xc * _LOG2E).astype(f32)
+    r = xc - n * _LN2_HI
+    r = r - n * _LN2_LO
+    p = _EXP_C[0]
+    for c in _EXP_C[1:]:
+        p = p * r + c
+    out = np.ldexp(p.astype(f32), n.astype(np.int32)).astype(f32)
+    return np.where(x < EXP_FLUSH, f32(0.0), out).astype(f32)
+
+
+def _butterfly(v):
+    """xor-butterfly over the last axis (64 lanes): off = 32, 16, ..., 1; returns lane 0."""
+    v = np.asarray(v, f32)
+    lanes = np.arange(v.shape[-1])
+    off = v.shape[-1] // 2
+    while off >= 1:
+        v = v + v[..., lanes ^ off]
+        off //= 2
+    return v[..., 0]
+
+
+def row_sum_lanesplit(x):
+    """Sum over the last axis in the 'strided' canonical order.
+
+    Lane l (0..63) accumulates x[l], x[l+64], x[l+128], ... starting from 0.0, then a
+    64-lane xor-butterfly.  Used for softmax and log-softmax denominators.
+    """
+    x = np.asarray(x, f32)
+    n = x.shape[-1]
+    t = -(-n // 64)
+    pad = np.zeros(x.shape[:-1] + (t * 64 - n,), f32)
+    xp = np.concatenate([x, pad], axis=-1).reshape(x.shape[:-1] + (t, 64))
+    acc = np.zeros(x.shape[:-1] + (64,), f32)
+    for i in range(t):
+        acc = acc + xp[..., i, :]
+    return _butterfly(acc)
+
+
+def row_sum_ln(x):
+    """Sum over a row of D (multiple of 256) in the LayerNorm canonical order.
+
+    Lane l owns the float4 chunks c = l, l+64, ... (elements 4c..4c+3); it sums its
+    elements sequentially (chunk order, then element order), then xor-butterfly.
+    """
+    x = np.asarray(x, f32)
+    D = x.shape[-1]
+    nch = D // 256
+    xc = x.reshape(x.shape[:-1] + (nch, 64, 4))
+    acc = xc[..., 0, :, 0]
+    for c in range(nch):
+        for e in range(4):
+            if c == 0 and e == 0:
+                continue
+            acc = acc + xc[..., c, :, e]
+    return _butterfly(acc)
+
+
+# ---------------------------------------------------------------------------------------
+# quantizers — quant_linear.py
+# ---------------------------------------------------------------------------------------
+
+def quant_rows(x, n_bits: int = 8):
+    """Per-row symmetric absmax quantizer.
+
+    quant_linear.py:30-43 (per-token activations) and quant_linear.py:5-17 (per output
+    channel weights) are the same formula on the last axis:
+    ``s = clamp(max|x|, 1e-5) / q_max``, ``q = round_half_even(x / s)``; the reference
+    returns ``q * s`` (fake quant), this returns the integers and the scale.
+    """
+    x = np.asarray(x, f32)
+    qmax = f32(2 ** (n_bits - 1) - 1)
+    s = np.maximum(np.abs(x).max(axis=-1), EPS_SCALE) / qmax
+    q = np.rint(x / s[..., None])
+    return q.astype(np.int8), s.astype(f32)
+
+
+def dequant(q, s):
+    """Fake-quant value ``q * s`` as the reference's quantizers return it."""
+    return (np.asarray(q, f32) * np.asarray(s, f32)[..., None]).astype(f32)
+
+
+def quant_weight(w, n_bits: int = 8):
+    """quant_linear.py:5-17 — per output channel (rows of the nn.Linear weight)."""
+    return quant_rows(w, n_bits)
+
+
+# ---------------------------------------------------------------------------------------
+# W8A8Linear — quant_linear.py:111-119
+# ---------------------------------------------------------------------------------------
+
+def int_gemm(qx, qw):
+    """Exact int32 accumulators acc[m, n] = sum_k qx[m, k] * qw[n, k]."""
+    a = np.asarray(qx, np.float64)
+    b = np.asarray(qw, np.float64)
+    acc = a @ b.T           # exact: |acc| <= K * 127^2 < 2^53
+    return acc.astype(np.int64).astype(np.int32)
+
+
+def linear_epilogue(acc, sx, sw, bias, relu=False):
+    """y = ((float(acc) * s_x[m]) * s_w[n]) + b[n]   (+ ReLU, position_feed_forward.py:12)."""
+    y = np.asarray(acc, np.int32).astype(f32)
+    y = y * np.asarray(sx, f32)[..., :, None]
+    y = y * np.asarray(sw, f32)
+    y = y + np.asarray(bias, f32)
+    if relu:
+        y = np.where(y > 0, y, f32(0.0)).astype(f32)
+    return y.astype(f32)
+
+
+class QLinear:
+    """Quantized weight of one W8A8Linear: int8 q [N, K], f32 s [N], f32 bias [N]."""
+
+    def __init__(self, w, b, n_bits=8):
+        self.q, self.s = quant_weight(w, n_bits)
+        self.b = np.asarray(b, f32)
+
+    def __call__(self, x, relu=False, quantize_output=False):
+        """W8A8Linear.forward (quant_linear.py:111-119) on an fp32 input x [..., K]."""
+        shp = x.shape
+        qx, sx = quant_rows(x.reshape(-1, shp[-1]))
+        y = linear_epilogue(int_gemm(qx, self.q), sx, self.s, self.b, relu=relu)
+        y = y.reshape(shp[:-1] + (y.shape[-1],))
+        if quantize_output:          # get_quantized_model.py:160-168 (Q/K/V)
+            return quant_rows(y)
+        return y
+
+
+# ---------------------------------------------------------------------------------------
+# LayerNorm — layer_norm.py:12-15 (unbiased std, eps added to std)
+# ---------------------------------------------------------------------------------------
+
+def layer_norm(x, a, b):
+    x = np.asarray(x, f32)
+    D = x.shape[-1]
+    mean = row_sum_ln(x) / f32(D)
+    d = x - mean[..., None]
+    var = row_sum_ln(d * d) / f32(D - 1)
+    std = np.sqrt(var).astype(f32)
+    den = std + LN_EPS
+    y = (np.asarray(a, f32) * d) / den[..., None]
+    return (y + np.asarray(b, f32)).astype(f32)
+
+
+# ---------------------------------------------------------------------------------------
+# attention — attention.py:23-36, on quantized Q/K/V (outputs of the QKV W8A8Linears)
+# ---------------------------------------------------------------------------------------
+
+def attention_scores(qq, sq, qk, sk, mask):
+    """scores[b,h,i,j] = ((float(acc) * s_q[i]) * s_k[j]) / 8, masked_fill(mask==0, -1e9).
+
+    qq [B,H,Sq,dk] int8, sq [B,Sq]; qk [B,H,Sk,dk], sk [B,Sk]; mask broadcastable to
+    [B,Sq,Sk] (nonzero = keep).
+    """
+    acc = np.einsum("bhid,bhjd->bhij", qq.astype(np.int64), qk.astype(np.int64))
+    s = acc.astype(np.int32).astype(f32)
+    s = s * np.asarray(sq, f32)[:, None, :, None]
+    s = s * np.asarray(sk, f32)[:, None, None, :]
+    s = s / f32(8.0) if qq.shape[-1] == 64 else s / f32(np.sqrt(qq.shape[-1]))
+    keep = np.broadcast_to(np.asarray(mask) != 0, (qq.shape[0], qq.shape[2], qk.shape[2]))
+    return np.where(keep[:, None], s, MASK_FILL).astype(f32)
+
+
+def softmax_quant(scores):
+    """softmax(-1) then P = round(P*127)/127 (attention.py:30,33-35). Returns int P*127."""
+    m = scores.max(axis=-1)
+    e = qexp(scores - m[..., None])
+    den = row_sum_lanesplit(e)
+    p = e / den[..., None]
+    return np.rint(p * f32(127.0)).astype(np.int8)
+
+
+def attention_pv(qp, qv, sv):
+    """ctx[b,h,i,d] = fma chain over j of (qp/127) * (float(qv) * s_v[j])."""
+    P = qp.astype(f32) / f32(127.0)                                 # [B,H,Sq,Sk]
+    V = qv.astype(f32) * np.asarray(sv, f32)[:, None, :, None]      # [B,H,Sk,dk]
+    B, H, Sq, Sk = P.shape
+    acc = np.zeros((B, H, Sq, V.shape[-1]), np.float64)
+    for j in range(Sk):
+        acc = (P[..., j, None].astype(np.float64) * V[:, :, j, None, :].astype(np.float64)
+               + acc).astype(f32).astype(np.float64)
+    return acc.astype(f32)
+
+
+def split_heads(q, H):
+    B, S, D = q.shape
+    return q.reshape(B, S, H, D // H).transpose(0, 2, 1, 3)
+
+
+def merge_heads(x):
+    B, H, S, dk = x.shape
+    return x.transpose(0, 2, 1, 3).reshape(B, S, H * dk)
+
+
+def attention(qq, sq, qk, sk, qv, sv, mask, H=8):
+    """Quantized Q/K/V [B,S,512] int8 + per-token scales -> ctx [B,Sq,512] f32, P ints."""
+    q4, k4, v4 = split_heads(qq, H), split_heads(qk, H), split_heads(qv, H)
+    scores = attention_scores(q4, sq, k4, sk, mask)
+    qp = softmax_quant(scores)
+    ctx = attention_pv(qp, v4, sv)
+    return merge_heads(ctx), qp
+
+
+# ---------------------------------------------------------------------------------------
+# model
+# ---------------------------------------------------------------------------------------
+
+class OracleModel:
+    """Quantized model restated from the reference modules (model.py:15-37)."""
+
+    def __init__(self, sd, n_layers=6, n_heads=8, n_bits=8):
+        self.N, self.H = n_layers, n_heads
+        L = lambda p: QLinear(sd[p + ".weight"], sd[p + ".bias"], n_bits)
+        Nm = lambda p: (np.asarray(sd[p + ".a_2"], f32), np.asarray(sd[p + ".b_2"], f32))
+        self.enc = []
+        for i in range(n_layers):
+            p = f"encoder.layers.{i}"
+            self.enc.append(dict(
+                attn=[L(f"{p}.self_attn.linears.{j}") for j in range(4)],
+                w1=L(f"{p}.feed_forward.w_1"), w2=L(f"{p}.feed_forward.w_2"),
+                ln=[Nm(f"{p}.sublayer.{j}.norm") for j in range(2)]))
+        self.enc_norm = Nm("encoder.norm")
+        self.dec = []
+        for i in range(n_layers):
+            p = f"decoder.layers.{i}"
+            self.dec.append(dict(
+                self_attn=[L(f"{p}.self_attn.linears.{j}") for j in range(4)],
+                src_attn=[L(f"{p}.src_attn.linears.{j}") for j in range(4)],
+                w1=L(f"{p}.feed_forward.w_1"), w2=L(f"{p}.feed_forward.w_2"),
+                ln=[Nm(f"{p}.sublayer.{j}.norm") for j in range(3)]))
+        self.dec_norm = Nm("decoder.norm")
+        self.src_lut = np.asarray(sd["src_embed.0.lut.weight"], f32)
+        self.tgt_lut = np.asarray(sd["tgt_embed.0.lut.weight"], f32)
+        self.pe = np.asarray(sd["src_embed.1.pe"], f32).reshape(-1, self.src_lut.shape[1])
+        self.gen_w = np.asarray(sd["generator.proj.weight"], f32)
+        self.gen_b = np.asarray(sd["generator.proj.bias"], f32)
+
+    # -- sublayers ---------------------------------------------------------------------
+    def mha(self, lin, xq, xkv, mask):
+        """MultiHeadedAttention.forward (attention.py:39-67)."""
+        qq, sq = lin[0](xq, quantize_output=True)
+        qk, sk = lin[1](xkv, quantize_output=True)
+        qv, sv = lin[2](xkv, quantize_output=True)
+        ctx, _ = attention(qq, sq, qk, sk, qv, sv, mask, self.H)
+        return lin[3](ctx)
+
+    def ffn(self, lp, x):
+        """PositionwiseFeedForward.forward (position_feed_forward.py:11-12)."""
+        return lp["w2"](lp["w1"](x, relu=True))
+
+    # -- stacks ------------------------------------------------------------------------
+    def encode(self, x, src_mask):
+        """Encoder.forward (encoder.py:14-18, 29-32). x [B,S,512], src_mask [B,1,S]."""
+        x = np.asarray(x, f32)
+        m = np.asarray(src_mask).reshape(x.shape[0], 1, -1)
+        for lp in self.enc:
+            h = layer_norm(x, *lp["ln"][0])
+            x = x + self.mha(lp["attn"], h, h, m)
+            x = x + self.ffn(lp, layer_norm(x, *lp["ln"][1]))
+        return layer_norm(x, *self.enc_norm)
+
+    def decode(self, y, memory, src_mask, tgt_mask):
+        """Decoder.forward (decoder.py:13-16, 28-33). tgt_mask [1|B,T,T]."""
+        x = np.asarray(y, f32)
+        B = x.shape[0]
+        sm = np.asarray(src_mask).reshape(B, 1, -1)
+        tm = np.broadcast_to(np.asarray(tgt_mask), (B,) + np.asarray(tgt_mask).shape[-2:])
+        for lp in self.dec:
+            h = layer_norm(x, *lp["ln"][0])
+            x = x + self.mha(lp["self_attn"], h, h, tm)
+            h = layer_norm(x, *lp["ln"][1])
+            x = x + self.mha(lp["src_attn"], h, memory, sm)
+            x = x + self.ffn(lp, layer_norm(x, *lp["ln"][2]))
+        return layer_norm(x, *self.dec_norm)
+
+    # -- host-side pieces of the decode loop ---------------------------------------------
+    def embed(self, ids, lut, pos0=0):
+        """Embeddings + PositionalEncoding (embeddings.py:12-13, positional_encodings.py:23-26)."""
+        ids = np.asarray(ids)
+        e = lut[ids] * f32(np.sqrt(512.0) if lut.shape[1] == 512 else np.sqrt(lut.shape[1]))
+        return (e + self.pe[pos0:pos0 + ids.shape[1]][None]).astype(f32)
+
+    def generator(self, x):
+        """Generator.forward (generator.py:14-15) + first-index argmax
+        (reference/onnx_reference_inference.py:640-641).  Returns (logprobs, ids)."""
+        x = np.asarray(x, f32)
+        acc = np.zeros((x.shape[0], self.gen_w.shape[0]), f32)
+        for k in range(x.shape[1]):
+            acc = fma32(x[:, k, None], self.gen_w[None, :, k], acc)
+        logits = acc + self.gen_b
+        m = logits.max(axis=-1)
+        z = logits - m[:, None]
+        lse = np.log(row_sum_lanesplit(qexp(z))).astype(f32)
+        lp = z - lse[:, None]
+        return lp.astype(f32), lp.argmax(axis=-1)
+
+    def greedy_decode(self, src, src_mask, max_len=72, start=0, kv_cache=True):
+        """Batched greedy decode (batch_output.py:659-673; B=1 form
+        reference/onnx_reference_inference.py:622-646): fixed max_len-1 steps, no EOS exit.
+
+        kv_cache=False recomputes the whole prefix each step exactly like the reference;
+        kv_cache=True computes only the new position (identical by causal invariance).
+        """
+        src = np.asarray(src)
+        B = src.shape[0]
+        memory = self.encode(self.embed(src, self.src_lut), src_mask)
+        ys = np.full((B, 1), start, np.int64)
+        if not kv_cache:
+            for _ in range(max_len - 1):
+                T = ys.shape[1]
+                out = self.decode(self.embed(ys, self.tgt_lut), memory, src_mask,
+                                  np.tril(np.ones((1, T, T), np.int64)))
+                _, nxt = self.generator(out[:, -1])
+                ys = np.concatenate([ys, nxt[:, None]], axis=1)
+            return ys
+        st = DecodeState(self, memory, src_mask, max_len)
+        for t in range(max_len - 1):
+            out = st.step(self.embed(ys[:, -1:], self.tgt_lut, pos0=t))
+            _, nxt = self.generator(out)
+            ys = np.concatenate([ys, nxt[:, None]], axis=1)
+        return ys
+
+
+class DecodeState:
+    """KV-cached decoder: self-attn K/V appended per step, cross K/V computed once."""
+
+    def __init__(self, model: OracleModel, memory, src_mask, max_len):
+        self.m = model
+        self.sm = np.asarray(src_mask).reshape(memory.shape[0], 1, -1)
+        self.cross = [(lp["src_attn"][1](memory, quantize_output=True),
+                       lp["src_attn"][2](memory, quantize_output=True)) for lp in model.dec]
+        self.kcache = [None] * model.N
+        self.vcache = [None] * model.N
+
+    def step(self, y):
+        """One new position per sentence: y [B,1,512] -> decoder output [B,512]."""
+        m = self.m
+        x = np.asarray(y, f32)
+        B = x.shape[0]
+        for L, lp in enumerate(m.dec):
+            h = layer_norm(x, *lp["ln"][0])
+            lin = lp["self_attn"]
+            qq, sq = lin[0](h, quantize_output=True)
+            k, v = lin[1](h, quantize_output=True), lin[2](h, quantize_output=True)
+            if self.kcache[L] is None:
+                self.kcache[L], self.vcache[L] = k, v
+            else:
+                self.kcache[L] = tuple(np.concatenate([a, b], 1) for a, b in zip(self.kcache[L], k))
+                self.vcache[L] = tuple(np.concatenate([a, b], 1) for a, b in zip(self.vcache[L], v))
+            (qk, sk), (qv, sv) = self.kcache[L], self.vcache[L]
+            ones = np.ones((B, 1, qk.shape[1]), np.int64)
+            ctx, _ = attention(qq, sq, qk, sk, qv, sv, ones, m.H)
+            x = x + lin[3](ctx)
+            h = layer_norm(x, *lp["ln"][1])
+            lin = lp["src_attn"]
+            qq, sq = lin[0](h, quantize_output=True)
+            (qk, sk), (qv, sv) = self.cross[L]
+            ctx, _ = attention(qq, sq, qk, sk, qv, sv, self.sm, m.H)
+            x = x + lin[3](ctx)
+            x = x + m.ffn(lp, layer_norm(x, *lp["ln"][2]))
+        return layer_norm(x, *m.dec_norm)[:, 0]
+
+
+def subsequent_mask(T):
+    """utils.py:10-14 / reference/onnx_reference_inference.py:649-655 as int64 [1,T,T]."""
+    return np.tril(np.ones((1, T, T), np.int64))

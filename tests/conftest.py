@@ -1,0 +1,48 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "onnx-transformer_amd")
+for p in (REPO, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a ROCm gfx950 GPU (MI355X)")
+
+
+@pytest.fixture(scope="session")
+def golden_ops():
+    return dict(np.load(os.path.join(GOLDEN, "golden_ops.npz")))
+
+
+@pytest.fixture(scope="session")
+def golden_model():
+    return dict(np.load(os.path.join(GOLDEN, "golden_model.npz")))
+
+
+@pytest.fixture(scope="session")
+def state_dict():
+    from qtx.weights import synthetic_state_dict
+    return synthetic_state_dict(20241223, ln_random=True)
+
+
+@pytest.fixture(scope="session")
+def oracle_model(state_dict):
+    from oracle.qtx_oracle import OracleModel
+    return OracleModel(state_dict)
+
+
+@pytest.fixture(scope="session")
+def gpu_model(state_dict):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from qtx.model import QtxModel
+    return QtxModel(state_dict)

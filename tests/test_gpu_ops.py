@@ -1,0 +1,151 @@
+"""Per-op parity of the HIP kernels (through the C-ABI) against the CPU oracle.
+
+Contract: bit-exact.  Integer tensors (quantized activations, int32-accumulator results,
+argmax ids) and the float outputs of the canonical evaluation order are compared with
+assert_array_equal; the only tolerance is the log-softmax value (platform log, 1 ulp).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import qtx_oracle as O
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def P(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def call(name, *args):
+    from qtx import _lib
+    _lib.call(name, *args)
+
+
+S0 = C.c_void_p(0)
+
+
+@pytest.mark.parametrize("D", [512, 2048])
+def test_row_quant(torch, D):
+    rng = np.random.default_rng(D)
+    x = (rng.standard_normal((37, D)) * rng.uniform(1e-3, 10, (37, 1))).astype(f32)
+    x[0] = 0
+    x[1, :4] = [127.0, 0.5, 1.5, -2.5]
+    x[1, 4:] = 0
+    xd = dev(torch, x)
+    q = torch.empty((37, D), dtype=torch.int8, device="cuda")
+    s = torch.empty((37,), dtype=torch.float32, device="cuda")
+    call("qtx_row_quant", P(xd), 37, D, 127.0, P(q), P(s), S0)
+    qo, so = O.quant_rows(x)
+    np.testing.assert_array_equal(q.cpu().numpy(), qo)
+    np.testing.assert_array_equal(s.cpu().numpy(), so)
+    call("qtx_row_quant", P(xd), 37, D, 7.0, P(q), P(s), S0)     # int4 weight quantizer
+    qo, so = O.quant_rows(x, 4)
+    np.testing.assert_array_equal(q.cpu().numpy(), qo)
+
+
+def test_layernorm_quant(torch, golden_ops, oracle_model):
+    x = golden_ops["ln_x"]
+    a, b = oracle_model.enc[0]["ln"][0]
+    y = torch.empty(x.shape, dtype=torch.float32, device="cuda")
+    q = torch.empty(x.shape, dtype=torch.int8, device="cuda")
+    s = torch.empty(x.shape[:1], dtype=torch.float32, device="cuda")
+    call("qtx_layernorm_quant", P(dev(torch, x)), P(dev(torch, a)), P(dev(torch, b)),
+         x.shape[0], 512, P(y), P(q), P(s), S0)
+    yo = O.layer_norm(x, a, b)
+    np.testing.assert_array_equal(y.cpu().numpy(), yo)
+    qo, so = O.quant_rows(yo)
+    np.testing.assert_array_equal(q.cpu().numpy(), qo)
+    np.testing.assert_array_equal(s.cpu().numpy(), so)
+
+
+@pytest.mark.parametrize("M,N,K,flags,bits", [
+    (16, 512, 512, 0, 8), (72, 1536, 512, 0, 8), (300, 512, 512, 2, 8),
+    (130, 2048, 512, 1, 8), (257, 512, 2048, 2, 8), (33, 512, 2048, 0, 4),
+    (512, 2048, 512, 1, 4)])
+def test_linear_i8(torch, M, N, K, flags, bits):
+    rng = np.random.default_rng(M * N + K)
+    x = rng.standard_normal((M, K)).astype(f32)
+    w = (rng.standard_normal((N, K)) * 0.05).astype(f32)
+    b = rng.standard_normal(N).astype(f32)
+    res = rng.standard_normal((M, N)).astype(f32)
+    qx, sx = O.quant_rows(x)
+    qw, sw = O.quant_weight(w, bits)
+    wd = dev(torch, qw)
+    if bits == 4:
+        packed = torch.empty((N, K // 2), dtype=torch.uint8, device="cuda")
+        call("qtx_pack_int4", P(wd), N, K, P(packed), S0)
+        wd = packed
+    out = dev(torch, res.copy()) if flags & 2 else torch.empty((M, N), dtype=torch.float32, device="cuda")
+    call("qtx_linear_i8", P(dev(torch, qx)), P(dev(torch, sx)), P(wd), P(dev(torch, sw)),
+         P(dev(torch, b)), M, N, K, bits, flags, P(out) if flags & 2 else S0, P(out), S0)
+    y = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b, relu=bool(flags & 1))
+    if flags & 2:
+        y = res + y
+    np.testing.assert_array_equal(out.cpu().numpy(), y)
+
+
+def test_linear_asymmetric_identity(torch):
+    """A = I-like, asymmetric W: catches row/col swaps of the MFMA C layout."""
+    M = N = K = 64 * 2
+    qx = np.zeros((M, K), np.int8)
+    qx[np.arange(M), np.arange(K)] = 1
+    qw = (np.arange(N * K).reshape(N, K) % 251 - 125).astype(np.int8)
+    one = np.ones(M, f32)
+    out = torch.empty((M, N), dtype=torch.float32, device="cuda")
+    call("qtx_linear_i8", P(dev(torch, qx)), P(dev(torch, one)), P(dev(torch, qw)),
+         P(dev(torch, np.ones(N, f32))), P(dev(torch, np.zeros(N, f32))), M, N, K, 8, 0, S0,
+         P(out), S0)
+    np.testing.assert_array_equal(out.cpu().numpy(), qw.T.astype(f32))
+
+
+@pytest.mark.parametrize("B,Sq,Sk,masked", [(2, 20, 20, True), (3, 1, 37, False),
+                                            (2, 128, 128, True), (1, 7, 300, True)])
+def test_attention(torch, B, Sq, Sk, masked):
+    rng = np.random.default_rng(Sq * 7 + Sk)
+    H = 8
+    q = rng.integers(-127, 128, (B, Sq, 512)).astype(np.int8)
+    k = rng.integers(-127, 128, (B, Sk, 512)).astype(np.int8)
+    v = rng.integers(-127, 128, (B, Sk, 512)).astype(np.int8)
+    sq, sk, sv = (rng.uniform(0.002, 0.03, (B, n)).astype(f32) for n in (Sq, Sk, Sk))
+    mask = np.ones((B, Sq, Sk), np.uint8)
+    if masked:
+        mask[-1, :, Sk // 2:] = 0
+        mask[0] = np.tril(np.ones((Sq, Sk), np.uint8), k=Sk - Sq)
+    ctx = torch.empty((B, Sq, 512), dtype=torch.float32, device="cuda")
+    call("qtx_attention_i8", P(dev(torch, q)), P(dev(torch, sq)), P(dev(torch, k)),
+         P(dev(torch, sk)), P(dev(torch, v)), P(dev(torch, sv)), P(dev(torch, mask)),
+         Sq * Sk, Sk, B, H, Sq, Sk, P(ctx), S0)
+    co, _ = O.attention(q, sq, k, sk, v, sv, mask, H)
+    np.testing.assert_array_equal(ctx.cpu().numpy(), co)
+
+
+def test_embed(torch, gpu_model, golden_ops, oracle_model):
+    ids = golden_ops["emb_ids"]
+    out = gpu_model.embed(dev(torch, ids), "src")
+    np.testing.assert_array_equal(out.cpu().numpy(), golden_ops["emb_ref"])
+    out = gpu_model.embed(dev(torch, ids[:, :5] % 4444), "tgt", pos0=9)
+    np.testing.assert_array_equal(out.cpu().numpy(),
+                                  oracle_model.embed(ids[:, :5] % 4444, oracle_model.tgt_lut, pos0=9))
+
+
+def test_generator(torch, gpu_model, golden_ops, oracle_model):
+    x = np.concatenate([golden_ops["gen_x"]] * 10)[:37]
+    logp, ids = gpu_model.generator(dev(torch, x))
+    lo, io = oracle_model.generator(x)
+    np.testing.assert_array_equal(ids.cpu().numpy(), io)
+    assert np.abs(logp.cpu().numpy() - lo).max() <= 2e-6
