@@ -4,7 +4,11 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -68,6 +72,14 @@ struct DecLayer {
   const float* ln[3][2];
 };
 
+struct GraphKey {
+  int B, S, L;
+  const void *ws, *ids, *mask;
+  bool operator<(const GraphKey& o) const {
+    return std::tie(B, S, L, ws, ids, mask) < std::tie(o.B, o.S, o.L, o.ws, o.ids, o.mask);
+  }
+};
+
 struct qtx_model {
   qtx_config cfg;
   std::vector<EncLayer> enc;
@@ -75,8 +87,18 @@ struct qtx_model {
   const float* enc_norm[2];
   const float* dec_norm[2];
   const float *src_lut, *tgt_lut, *pe, *gen_w, *gen_b;
+  float* gen_wt = nullptr;   // generator weight transposed [d_model][tgt_vocab]
   void* mem = nullptr;
   size_t bytes = 0;
+  // decode-step graphs, keyed by shape and the buffers baked into them
+  std::mutex mu;
+  hipStream_t gstream = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  std::map<GraphKey, hipGraphExec_t> graphs;
+  void clear_graphs() {
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    graphs.clear();
+  }
 };
 
 namespace {
@@ -175,6 +197,7 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     float* gw = ar.take<float>((size_t)c.tgt_vocab * D);
     float* gb = ar.take<float>(c.tgt_vocab);
     int8_t* tmp = ar.take<int8_t>((size_t)F * D);
+    m->gen_wt = ar.take<float>((size_t)c.tgt_vocab * D);
     return std::make_tuple(norms, src_lut, tgt_lut, pe_d, gw, gb, tmp);
   };
   qtx_model* m = new qtx_model();
@@ -249,6 +272,8 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     if (he != hipSuccess) { qtx_model_destroy(m); return fail(QTX_E_HIP, "copy tables"); }
   }
   m->src_lut = src_lut; m->tgt_lut = tgt_lut; m->pe = pe_d; m->gen_w = gw; m->gen_b = gb;
+  he = launch_transpose(gw, c.tgt_vocab, D, m->gen_wt, st);
+  if (he != hipSuccess) { qtx_model_destroy(m); return fail(QTX_E_HIP, "transpose generator"); }
   he = hipStreamSynchronize(st);
   if (he != hipSuccess) {
     qtx_model_destroy(m);
@@ -260,6 +285,11 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
 
 int32_t qtx_model_destroy(qtx_model* m) {
   if (!m) return QTX_OK;
+  if (m->gstream) (void)hipStreamSynchronize(m->gstream);
+  m->clear_graphs();
+  if (m->ev_in) (void)hipEventDestroy(m->ev_in);
+  if (m->ev_out) (void)hipEventDestroy(m->ev_out);
+  if (m->gstream) (void)hipStreamDestroy(m->gstream);
   if (m->mem) (void)hipFree(m->mem);
   delete m;
   return QTX_OK;
@@ -481,7 +511,8 @@ struct GreedyWS {
   float* memory;
   float* xo;
   float* logits;
-  int* step;
+  int* step;          // [0] = decode position, [1] = argmax arrival counter
+  unsigned* rowmax;   // [B] FFN1 row absmax (A_F32Q operand of FFN2)
 };
 
 GreedyWS carve_greedy(Arena& ar, const qtx_config& c, int B, int S, int max_len) {
@@ -500,7 +531,141 @@ GreedyWS carve_greedy(Arena& ar, const qtx_config& c, int B, int S, int max_len)
   g.xo = ar.take<float>((size_t)B * D);
   g.logits = ar.take<float>((size_t)B * c.tgt_vocab);
   g.step = ar.take<int>(4);
+  g.rowmax = ar.take<unsigned>((size_t)B);
   return g;
+}
+
+bool env_flag(const char* name);
+
+// ---- fused decode step (M = B rows, keys <= 128) ----------------------------------------
+SkinnyArgs skinny(int wbits, const QLin& L, int M, int amode, int flags, float* out, long ldo) {
+  SkinnyArgs s{};
+  s.amode = amode; s.W = L.q; s.ldw = wbits == 8 ? L.K : L.K / 2; s.sw = L.s; s.bias = L.b;
+  s.out = out; s.ldo = ldo; s.M = M; s.N = L.N; s.K = L.K; s.flags = flags;
+  return s;
+}
+
+// One KV-cached decoder step for every sentence, 8 kernels per layer + 2:
+//   [LN+QKV] [self-attn] [O+res] [LN+Qc] [cross-attn] [Oc+res] [LN+FFN1+relu] [FFN2+res]
+//   [final LN + generator] [log_softmax/argmax + next embedding + step++]
+// Reads the position from g.step (device), so it can be captured once and replayed.
+int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len,
+                      int64_t* ids, const uint8_t* src_mask, hipStream_t st) {
+  const qtx_config& c = m->cfg;
+  const int D = c.d_model, F = c.d_ff, wb = c.weight_bits;
+  const bool ffn_rowmax = env_flag("QTX_FFN_ROWMAX");
+  const bool fused_ln = env_flag("QTX_FUSED_LN");
+  Scratch& s = g.dec;
+  // out = epilogue(quant(LN(x)) . W^T): LayerNorm + per-token quant as its own kernel
+  // (one wave per row, 2.7 us) then the int8 GEMM — measured faster than recomputing the
+  // LayerNorm of all rows in every GEMM workgroup (the A_LN prologue, QTX_FUSED_LN=1).
+  auto ln_linear = [&](const QLin& W, const float* const* ln, int flags, float* out,
+                       long ldo) -> int {
+    SkinnyArgs k = skinny(wb, W, B, fused_ln ? A_LN : A_I8, flags, out, ldo);
+    if (fused_ln) {
+      k.X = s.x; k.ldx = D; k.ln_a = ln[0]; k.ln_b = ln[1];
+    } else {
+      RC(ln_quant(s.x, B, ln, D, s.a8, s.sa, st));
+      k.A = s.a8; k.sa = s.sa;
+    }
+    HIPCHK(launch_skinny(k, wb, st));
+    return QTX_OK;
+  };
+  for (int l = 0; l < c.n_layers; ++l) {
+    const DecLayer& L = m->dec[l];
+    SkinnyArgs a;
+    RC(ln_linear(L.qkv, L.ln[0], 0, s.y, 3 * D));
+    DecAttnArgs at{};
+    at.y = s.y; at.ldy = 3 * D; at.kv_new = 1; at.step = g.step;
+    at.kc = g.kc[l]; at.vc = g.vc[l]; at.skc = g.skc[l]; at.svc = g.svc[l]; at.kv_bs = max_len;
+    at.a8 = s.a8; at.sa = s.sa;
+    HIPCHK(launch_dec_attn(at, B, st));
+    a = skinny(wb, L.o, B, A_I8, EPI_RESIDUAL, s.x, D);
+    a.A = s.a8; a.sa = s.sa; a.res = s.x; a.ldr = D;
+    HIPCHK(launch_skinny(a, wb, st));
+    RC(ln_linear(L.cq, L.ln[1], 0, s.y, D));
+    at = DecAttnArgs{};
+    at.y = s.y; at.ldy = D; at.kv_new = 0; at.S = S; at.mask = src_mask;
+    at.kc = g.cross.k8[l]; at.vc = g.cross.v8[l]; at.skc = g.cross.sk[l];
+    at.svc = g.cross.sv[l]; at.kv_bs = S;
+    at.a8 = s.a8; at.sa = s.sa;
+    HIPCHK(launch_dec_attn(at, B, st));
+    a = skinny(wb, L.co, B, A_I8, EPI_RESIDUAL, s.x, D);
+    a.A = s.a8; a.sa = s.sa; a.res = s.x; a.ldr = D;
+    a.zero = g.rowmax; a.zero_n = B;
+    HIPCHK(launch_skinny(a, wb, st));
+    if (ffn_rowmax) {   // FFN2 quantizes h itself from FFN1's atomic row maxima
+      a = skinny(wb, L.w1, B, A_LN, EPI_RELU | EPI_ROWMAX, s.y, F);
+      a.X = s.x; a.ldx = D; a.ln_a = L.ln[2][0]; a.ln_b = L.ln[2][1]; a.rowmax_out = g.rowmax;
+      HIPCHK(launch_skinny(a, wb, st));
+      a = skinny(wb, L.w2, B, A_F32Q, EPI_RESIDUAL, s.x, D);
+      a.X = s.y; a.ldx = F; a.rowmax_in = g.rowmax; a.res = s.x; a.ldr = D;
+      HIPCHK(launch_skinny(a, wb, st));
+    } else {            // one wave per row quantizes h (quant_linear.py:30-43), then FFN2
+      RC(ln_linear(L.w1, L.ln[2], EPI_RELU, s.y, F));
+      RC(quant(s.y, F, B, F, s.a8, s.sa, st));
+      a = skinny(wb, L.w2, B, A_I8, EPI_RESIDUAL, s.x, D);
+      a.A = s.a8; a.sa = s.sa; a.res = s.x; a.ldr = D;
+      HIPCHK(launch_skinny(a, wb, st));
+    }
+  }
+  if (getenv("QTX_DBG_TAIL")) {   // bisection aid: reference-shaped tail kernels
+    RC(ln_out(s.x, B, m->dec_norm, D, g.xo, st));
+    HIPCHK(launch_generator(g.xo, D, B, m->gen_w, m->gen_b, c.tgt_vocab, g.logits, st));
+    HIPCHK(launch_logsoftmax_argmax(g.logits, B, c.tgt_vocab, nullptr, ids, max_len, g.step,
+                                    1, st));
+    HIPCHK(launch_step_inc(g.step, st));
+    HIPCHK(launch_embed(ids, max_len, B, 1, g.step, 0, m->tgt_lut, c.tgt_vocab, m->pe,
+                        c.max_len, s.x, D, st));
+    return QTX_OK;
+  }
+  HIPCHK(launch_generator_mfma(s.x, D, B, m->dec_norm[0], m->dec_norm[1], m->gen_wt, m->gen_b,
+                               c.tgt_vocab, g.logits, st));
+  HIPCHK(launch_argmax_embed(g.logits, B, c.tgt_vocab, ids, max_len, g.step,
+                             reinterpret_cast<unsigned*>(g.step + 1), m->tgt_lut, m->pe,
+                             c.max_len, s.x, st));
+  return QTX_OK;
+}
+
+// The reference-shaped unfused step (any key count up to 512).
+int greedy_step_unfused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len,
+                        int64_t* ids, const uint8_t* src_mask, hipStream_t st) {
+  const qtx_config& c = m->cfg;
+  const int D = c.d_model;
+  Scratch& s = g.dec;
+  HIPCHK(launch_embed(ids, max_len, B, 1, g.step, 0, m->tgt_lut, c.tgt_vocab, m->pe,
+                      c.max_len, s.x, D, st));
+  for (int l = 0; l < c.n_layers; ++l) {
+    const DecLayer& L = m->dec[l];
+    RC(ln_quant(s.x, B, L.ln[0], D, s.a8, s.sa, st));
+    RC(linear(c, L.qkv, s.a8, s.sa, B, 0, nullptr, s.y, 3 * D, st));
+    RC(quant(s.y, 3 * D, B, D, s.q8, s.sq, st));
+    RowArgs kr = rows_quant(s.y + D, 3 * D, B, D, g.kc[l], g.skc[l]);
+    kr.rpb = 1; kr.dst_bstride = max_len; kr.dst_off_dev = g.step;
+    HIPCHK(launch_rows(kr, st));
+    RowArgs vr = rows_quant(s.y + 2 * D, 3 * D, B, D, g.vc[l], g.svc[l]);
+    vr.rpb = 1; vr.dst_bstride = max_len; vr.dst_off_dev = g.step;
+    HIPCHK(launch_rows(vr, st));
+    AttnArgs a = attn_args(s, B, 1, 0, max_len);
+    a.k = g.kc[l]; a.sk = g.skc[l]; a.v = g.vc[l]; a.sv = g.svc[l];
+    a.sk_dev = g.step; a.sk_add = 1;
+    HIPCHK(launch_attention(a, st));
+    RC(quant(s.ctx, D, B, D, s.a8, s.sa, st));
+    RC(linear(c, L.o, s.a8, s.sa, B, EPI_RESIDUAL, s.x, s.x, D, st));
+    RC(cross_attn_block(m, L, l, s, g.cross, B, 1, S, src_mask, st));
+    RC(ffn_block(c, L.w1, L.w2, L.ln[2], s, B, st));
+  }
+  RC(ln_out(s.x, B, m->dec_norm, D, g.xo, st));
+  HIPCHK(launch_generator(g.xo, D, B, m->gen_w, m->gen_b, c.tgt_vocab, g.logits, st));
+  HIPCHK(launch_logsoftmax_argmax(g.logits, B, c.tgt_vocab, nullptr, ids, max_len, g.step, 1,
+                                  st));
+  HIPCHK(launch_step_inc(g.step, st));
+  return QTX_OK;
+}
+
+bool env_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && *v && strcmp(v, "0") != 0;
 }
 
 }  // namespace
@@ -579,8 +744,9 @@ int32_t qtx_generator(const qtx_model* m, const float* x, int32_t M, float* logp
   const int V = m->cfg.tgt_vocab;
   if (ws_bytes < (size_t)M * V * sizeof(float)) return fail(QTX_E_WORKSPACE, "ws too small");
   hipStream_t st = (hipStream_t)stream;
-  float* logits = (float*)ws;
-  HIPCHK(launch_generator(x, m->cfg.d_model, M, m->gen_w, m->gen_b, V, logits, st));
+  float* logits = (float*)ws;   // the raw logits stay in ws[0 .. M*V) for the caller
+  HIPCHK(launch_generator_mfma(x, m->cfg.d_model, M, nullptr, nullptr, m->gen_wt, m->gen_b, V,
+                               logits, st));
   HIPCHK(launch_logsoftmax_argmax(logits, M, V, logp, ids, 1, nullptr, 0, st));
   return QTX_OK;
 }
@@ -607,41 +773,55 @@ int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t*
   RC(encoder_run(m, g.enc.x, src_mask, B, S, g.memory, g.enc, st));
   RC(cross_kv(m, g.memory, B * S, g.cross, st));
 
-  // ids[:, 0] = start ; step counter = 0
+  // ids[:, 0] = start ; step[0] = position 0, step[1] = arrival counter
   HIPCHK(launch_fill_col(ids, max_len, B, start, st));
   HIPCHK(hipMemsetAsync(g.step, 0, 16, st));
-  Scratch& s = g.dec;
-  for (int t = 0; t + 1 < max_len; ++t) {
-    // x = tgt_embed(ys[:, step]) at position step
-    HIPCHK(launch_embed(ids, max_len, B, 1, g.step, 0, m->tgt_lut, c.tgt_vocab, m->pe,
-                        c.max_len, s.x, D, st));
-    for (int l = 0; l < c.n_layers; ++l) {
-      const DecLayer& L = m->dec[l];
-      // masked self-attention with KV cache
-      RC(ln_quant(s.x, B, L.ln[0], D, s.a8, s.sa, st));
-      RC(linear(c, L.qkv, s.a8, s.sa, B, 0, nullptr, s.y, 3 * D, st));
-      RC(quant(s.y, 3 * D, B, D, s.q8, s.sq, st));
-      RowArgs kr = rows_quant(s.y + D, 3 * D, B, D, g.kc[l], g.skc[l]);
-      kr.rpb = 1; kr.dst_bstride = max_len; kr.dst_off_dev = g.step;
-      HIPCHK(launch_rows(kr, st));
-      RowArgs vr = rows_quant(s.y + 2 * D, 3 * D, B, D, g.vc[l], g.svc[l]);
-      vr.rpb = 1; vr.dst_bstride = max_len; vr.dst_off_dev = g.step;
-      HIPCHK(launch_rows(vr, st));
-      AttnArgs a = attn_args(s, B, 1, 0, max_len);
-      a.k = g.kc[l]; a.sk = g.skc[l]; a.v = g.vc[l]; a.sv = g.svc[l];
-      a.sk_dev = g.step; a.sk_add = 1;
-      HIPCHK(launch_attention(a, st));
-      RC(quant(s.ctx, D, B, D, s.a8, s.sa, st));
-      RC(linear(c, L.o, s.a8, s.sa, B, EPI_RESIDUAL, s.x, s.x, D, st));
-      RC(cross_attn_block(m, L, l, s, g.cross, B, 1, S, src_mask, st));
-      RC(ffn_block(c, L.w1, L.w2, L.ln[2], s, B, st));
-    }
-    RC(ln_out(s.x, B, m->dec_norm, D, g.xo, st));
-    HIPCHK(launch_generator(g.xo, D, B, m->gen_w, m->gen_b, c.tgt_vocab, g.logits, st));
-    HIPCHK(launch_logsoftmax_argmax(g.logits, B, c.tgt_vocab, nullptr, ids, max_len, g.step, 1,
-                                    st));
-    HIPCHK(launch_step_inc(g.step, st));
+  const bool fused = S <= 128 && max_len <= 128 && !env_flag("QTX_UNFUSED");
+  if (!fused) {
+    for (int t = 0; t + 1 < max_len; ++t) RC(greedy_step_unfused(m, g, B, S, max_len, ids, src_mask, st));
+    return QTX_OK;
   }
+  // first decoder input: tgt_embed(ys[:, 0]) at position 0; later ones come from the
+  // argmax kernel of the previous step
+  HIPCHK(launch_embed(ids, max_len, B, 1, g.step, 0, m->tgt_lut, c.tgt_vocab, m->pe,
+                      c.max_len, g.dec.x, D, st));
+  if (env_flag("QTX_NO_GRAPH")) {
+    for (int t = 0; t + 1 < max_len; ++t) RC(greedy_step_fused(m, g, B, S, max_len, ids, src_mask, st));
+    return QTX_OK;
+  }
+  // One decode step captured once per (shape, buffers) as a hipGraph and replayed
+  // max_len-1 times on the model's stream, ordered after / before the caller's stream.
+  qtx_model* mm = const_cast<qtx_model*>(m);
+  std::lock_guard<std::mutex> lock(mm->mu);
+  if (!mm->gstream) {
+    HIPCHK(hipStreamCreateWithFlags(&mm->gstream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&mm->ev_in, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&mm->ev_out, hipEventDisableTiming));
+  }
+  const GraphKey key{B, S, max_len, ws, ids, src_mask};
+  auto it = mm->graphs.find(key);
+  if (it == mm->graphs.end()) {
+    if (mm->graphs.size() >= 16) mm->clear_graphs();
+    hipGraph_t graph = nullptr;
+    HIPCHK(hipStreamBeginCapture(mm->gstream, hipStreamCaptureModeThreadLocal));
+    const int rc = greedy_step_fused(m, g, B, S, max_len, ids, src_mask, mm->gstream);
+    const hipError_t ec = hipStreamEndCapture(mm->gstream, &graph);
+    if (rc != QTX_OK) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    HIPCHK(ec);
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    HIPCHK(ei);
+    it = mm->graphs.emplace(key, exec).first;
+  }
+  HIPCHK(hipEventRecord(mm->ev_in, st));
+  HIPCHK(hipStreamWaitEvent(mm->gstream, mm->ev_in, 0));
+  for (int t = 0; t + 1 < max_len; ++t) HIPCHK(hipGraphLaunch(it->second, mm->gstream));
+  HIPCHK(hipEventRecord(mm->ev_out, mm->gstream));
+  HIPCHK(hipStreamWaitEvent(st, mm->ev_out, 0));
   return QTX_OK;
 }
 
@@ -684,6 +864,44 @@ int32_t qtx_linear_i8(const int8_t* A, const float* sa, const void* W, const flo
   hipError_t e = launch_gemm(g, weight_bits, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "weight_bits=%d", weight_bits);
   HIPCHK(e);
+  return QTX_OK;
+}
+
+int32_t qtx_skinny_linear(int32_t amode, const int8_t* A, const float* sa, const float* X,
+                          int64_t ldx, const float* ln_a, const float* ln_b,
+                          const uint32_t* rowmax_in, const void* W, const float* sw,
+                          const float* bias, int32_t M, int32_t N, int32_t K,
+                          int32_t weight_bits, int32_t flags, const float* res, float* out,
+                          uint32_t* rowmax_out, void* stream) {
+  if (!W || !sw || !bias || !out) return fail(QTX_E_INVALID, "null argument");
+  if ((amode == A_I8 && (!A || !sa)) || (amode == A_LN && (!X || !ln_a || !ln_b)) ||
+      (amode == A_F32Q && (!X || !rowmax_in)) || amode < 0 || amode > 2)
+    return fail(QTX_E_INVALID, "operands missing for amode %d", amode);
+  if (((flags & EPI_RESIDUAL) && !res) || ((flags & EPI_ROWMAX) && !rowmax_out))
+    return fail(QTX_E_INVALID, "flags need res / rowmax_out");
+  SkinnyArgs g{};
+  g.amode = amode; g.A = A; g.sa = sa; g.X = X; g.ldx = ldx; g.ln_a = ln_a; g.ln_b = ln_b;
+  g.rowmax_in = rowmax_in; g.W = (const int8_t*)W; g.ldw = weight_bits == 8 ? K : K / 2;
+  g.sw = sw; g.bias = bias; g.out = out; g.ldo = N; g.res = res; g.ldr = N;
+  g.rowmax_out = rowmax_out; g.M = M; g.N = N; g.K = K; g.flags = flags;
+  hipError_t e = launch_skinny(g, weight_bits, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue)
+    return fail(QTX_E_UNSUPPORTED, "skinny: N=%d K=%d amode=%d bits=%d", N, K, amode, weight_bits);
+  HIPCHK(e);
+  return QTX_OK;
+}
+
+int32_t qtx_decode_attention(int32_t kv_new, const float* y, int64_t ldy, int8_t* kc,
+                             int8_t* vc, float* skc, float* svc, int32_t kv_bs,
+                             const int32_t* step_dev, int32_t S, const uint8_t* mask,
+                             int32_t B, int8_t* a8, float* sa, void* stream) {
+  if (!y || !kc || !vc || !skc || !svc || !a8 || !sa) return fail(QTX_E_INVALID, "null argument");
+  if (kv_new ? !step_dev : (!mask || S <= 0 || S > 128 || S > kv_bs))
+    return fail(QTX_E_INVALID, "decode attention: bad step/mask/S");
+  DecAttnArgs a{};
+  a.y = y; a.ldy = ldy; a.kc = kc; a.vc = vc; a.skc = skc; a.svc = svc; a.kv_bs = kv_bs;
+  a.step = step_dev; a.S = S; a.mask = mask; a.a8 = a8; a.sa = sa; a.kv_new = kv_new;
+  HIPCHK(launch_dec_attn(a, B, (hipStream_t)stream));
   return QTX_OK;
 }
 

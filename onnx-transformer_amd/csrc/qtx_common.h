@@ -16,17 +16,34 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 namespace qtx {
 
 // ---------------------------------------------------------------- wave reductions
-// xor-butterfly, offsets 32,16,8,4,2,1.  Lane l adds its partner l^off; fp32 addition
-// is commutative, so every lane ends with the same value as lane 0.
+// Canonical sum of 64 lane values = the balanced pairwise tree over lanes in natural
+// order: ((l0+l1)+(l2+l3)) ... — what an xor-butterfly computes in every lane.
+// Implemented with DPP (VALU, no LDS round trip): xor1 / xor2 by quad_perm, then
+// half-mirror (pairs the two quads of an 8-lane group) and mirror (the two octets of a
+// 16-lane row) — once groups are uniform a mirror pairs the same two partial sums as an
+// xor would — and the four row sums combined as (r0 + r1) + (r2 + r3) via readlane.
+// fp32 addition is commutative, so the result is bit-identical to the oracle's
+// butterfly (oracle/qtx_oracle.py:_butterfly).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
-  return v;
+  v = v + dpp<0xB1>(v);    // quad_perm [1,0,3,2]  (xor 1)
+  v = v + dpp<0x4E>(v);    // quad_perm [2,3,0,1]  (xor 2)
+  v = v + dpp<0x141>(v);   // row_half_mirror      (xor 4 on uniform quads)
+  v = v + dpp<0x140>(v);   // row_mirror           (xor 8 on uniform octets)
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-  return v;
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  v = fmaxf(v, dpp<0x140>(v));
+  return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 
 // ---------------------------------------------------------------- canonical exp
@@ -51,6 +68,25 @@ __device__ __forceinline__ float qexp(float x) {
   return x < -80.0f ? 0.0f : e;
 }
 
+// ---------------------------------------------------------------- shared-divisor division
+// Correctly rounded a / b for many a sharing one divisor b (Markstein): with
+// y = RN(1/b), q = RN(a*y), r = fma(-q, b, a) (exact), RN(q + r*y) == RN(a/b) provided
+// nothing over/underflows.  div_ok() is that range guard; callers vote it over the wave
+// and take the true division when any lane is outside (tools/ + DESIGN.md §3).
+__device__ __forceinline__ float div_cr(float a, float b, float y) {
+  const float q = a * y;
+  const float r = fmaf(-q, b, a);
+  return fmaf(r, y, q);
+}
+__device__ __forceinline__ bool div_ok(float a) {
+  const float m = fabsf(a);
+  return m == 0.0f || (m > 0x1p-60f && m < 0x1p60f);
+}
+__device__ __forceinline__ bool divisor_ok(float b) {
+  const float m = fabsf(b);
+  return m > 0x1p-30f && m < 0x1p30f;
+}
+
 // ---------------------------------------------------------------- quantizer
 // quant_linear.py:30-43 / :5-17:  s = max(absmax, 1e-5) / qmax;  q = rint(x / s).
 __device__ __forceinline__ float quant_scale(float absmax, float qmax) {
@@ -62,6 +98,40 @@ __device__ __forceinline__ int quant_val(float x, float s) { return (int)rintf(x
 __device__ __forceinline__ uint32_t pack4_i8(int a, int b, int c, int d) {
   return (uint32_t)(a & 0xff) | ((uint32_t)(b & 0xff) << 8) | ((uint32_t)(c & 0xff) << 16) |
          ((uint32_t)(d & 0xff) << 24);
+}
+
+// rint(x / s) with the correctly rounded quotient, computed as x * (1/s) except within
+// 2^-13 of a rounding tie, where the true division is taken.  Exact: |x/s| <= ~127, so
+// the reciprocal product is within 2^-16 of x/s and fl(x/s) within 2^-18; away from a
+// tie both round to the same integer.
+// The near-tie test is folded over all of a lane's values and voted across the wave, so
+// the division runs behind ONE wave-uniform branch that is almost never taken.
+template <int N>
+__device__ __forceinline__ void quant_pack(const float* x, float s, uint32_t* out) {
+  static_assert(N % 4 == 0, "groups of 4");
+  const float inv = 1.0f / s;
+  float r[N];
+  bool near = false;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    r[i] = x[i] * inv;
+    near |= fabsf((r[i] - floorf(r[i])) - 0.5f) < 0x1p-13f;
+  }
+  if (__builtin_expect(__ballot(near) != 0ull, 0)) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) r[i] = x[i] / s;
+  }
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i)
+    out[i] = pack4_i8((int)rintf(r[4 * i]), (int)rintf(r[4 * i + 1]), (int)rintf(r[4 * i + 2]),
+                      (int)rintf(r[4 * i + 3]));
+}
+// single value per lane
+__device__ __forceinline__ int quant_one(float x, float s) {
+  float r = x * (1.0f / s);
+  const bool near = fabsf((r - floorf(r)) - 0.5f) < 0x1p-13f;
+  if (__builtin_expect(__ballot(near) != 0ull, 0)) r = x / s;
+  return (int)rintf(r);
 }
 
 // |x| as an order-preserving uint (for atomicMax on non-negative floats)

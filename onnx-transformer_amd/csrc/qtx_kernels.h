@@ -25,6 +25,46 @@ struct GemmArgs {
   int flags;
 };
 
+// Skinny (decode) GEMM: M <= 64 rows per workgroup, 16 output columns per workgroup,
+// the 4 waves split K and reduce their exact int32 partials through LDS.
+// The A operand is produced in the prologue according to amode:
+enum : int {
+  A_I8 = 0,    // int8 A [M,K] + sa[M]
+  A_LN = 1,    // fp32 X [M,512]: LayerNorm(ln_a, ln_b) + per-token quant in the prologue
+  A_F32Q = 2,  // fp32 X [M,K] + rowmax bits [M]: quant with s = max(rowmax,1e-5)/127
+};
+enum : int {
+  EPI_ROWMAX = 4,  // atomicMax(rowmax_out[m], bits(|y|)) after the other flags
+};
+struct SkinnyArgs {
+  int amode;
+  const int8_t* A; const float* sa;               // A_I8
+  const float* X; long ldx;                       // A_LN / A_F32Q
+  const float* ln_a; const float* ln_b;           // A_LN
+  const unsigned* rowmax_in;                      // A_F32Q
+  const int8_t* W; long ldw; const float* sw; const float* bias;
+  float* out; long ldo; const float* res; long ldr;
+  unsigned* rowmax_out;                           // EPI_ROWMAX
+  unsigned* zero; int zero_n;                     // block (0,0) zeroes zero[0..n) (side task)
+  int M, N, K, flags;
+};
+
+// Fused decode attention: one workgroup (8 waves = 8 heads) per sentence b, one query.
+//   self  (kv_new != 0): q/k/v rows from y [B, 3*512] fp32 are quantized per token;
+//                        k/v appended to the caches at position *step; keys 0..*step.
+//   cross (kv_new == 0): q row from y [B, 512]; keys = the S cached cross K/V rows,
+//                        masked by mask[b*S + j].
+//   Both quantize the context row per token into a8/sa (the next GEMM's A operand).
+struct DecAttnArgs {
+  const float* y; long ldy;
+  int8_t* kc; int8_t* vc; float* skc; float* svc; long kv_bs;   // [B][kv_bs rows][512]
+  const int* step;            // self: current position
+  int S;                      // cross: number of keys
+  const uint8_t* mask;        // cross: [B, S]
+  int8_t* a8; float* sa;      // out: quantized context [B, 512] + scale
+  int kv_new;
+};
+
 // Row quantizer / LayerNorm+quantizer over rows of D floats (one wave per row).
 //   x row r at x + r*ldx.  If ln_a: y = LN(x) (layer_norm.py:12-15) else y = x.
 //   If yout: yout row r = y (fp32).   If q: quantize y per row (quant_linear.py:30-43)
@@ -52,6 +92,23 @@ struct AttnArgs {
 };
 
 hipError_t launch_gemm(const GemmArgs& a, int wbits, hipStream_t st);
+hipError_t launch_skinny(const SkinnyArgs& a, int wbits, hipStream_t st);
+hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st);
+// generator with the final LayerNorm fused in (ln_a may be null = no LN)
+hipError_t launch_generator_ln(const float* x, long ldx, int M, const float* ln_a,
+                               const float* ln_b, const float* W, const float* b, int V,
+                               float* logits, hipStream_t st);
+// the same on fp32 MFMA (bit-identical chain); Wt = generator weight transposed [512][V]
+hipError_t launch_generator_mfma(const float* x, long ldx, int M, const float* ln_a,
+                                 const float* ln_b, const float* Wt, const float* b, int V,
+                                 float* logits, hipStream_t st);
+hipError_t launch_transpose(const float* in, int R, int C, float* out, hipStream_t st);
+// log_softmax + argmax + next-token embedding + step increment (decode tail):
+//   ids[m, *step + 1] = argmax;  xnext[m] = lut[id]*sqrt(512) + pe[*step + 1];
+//   the last workgroup to finish advances *step (arrive is its private counter).
+hipError_t launch_argmax_embed(const float* logits, int M, int V, int64_t* ids, long ids_bs,
+                               int* step, unsigned* arrive, const float* lut, const float* pe,
+                               int max_pos, float* xnext, hipStream_t st);
 hipError_t launch_rows(const RowArgs& a, hipStream_t st);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st);
 hipError_t launch_embed(const int64_t* ids, long ids_bs, int B, int T, const int* pos_dev,

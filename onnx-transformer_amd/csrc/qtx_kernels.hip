@@ -52,14 +52,30 @@ __global__ __launch_bounds__(256) void k_rows(RowArgs a) {
         if (c | e) ss = ss + d[c][e] * d[c][e];
     const float var = wave_sum(ss) / (D - 1.0f);
     const float den = sqrtf(var) + 1e-6f;
+    float gb[NCH][4];
+    bool ok = divisor_ok(den);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const float4 ga = *reinterpret_cast<const float4*>(a.ln_a + 4 * (lane + 64 * c));
-      const float4 gb = *reinterpret_cast<const float4*>(a.ln_b + 4 * (lane + 64 * c));
-      v[c][0] = (ga.x * d[c][0]) / den + gb.x;
-      v[c][1] = (ga.y * d[c][1]) / den + gb.y;
-      v[c][2] = (ga.z * d[c][2]) / den + gb.z;
-      v[c][3] = (ga.w * d[c][3]) / den + gb.w;
+      const float4 tb = *reinterpret_cast<const float4*>(a.ln_b + 4 * (lane + 64 * c));
+      d[c][0] = ga.x * d[c][0]; d[c][1] = ga.y * d[c][1];
+      d[c][2] = ga.z * d[c][2]; d[c][3] = ga.w * d[c][3];
+      gb[c][0] = tb.x; gb[c][1] = tb.y; gb[c][2] = tb.z; gb[c][3] = tb.w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ok &= div_ok(d[c][e]);
+    }
+    // (a * d) / den: correctly rounded via div_cr unless a value is out of its range
+    if (__builtin_expect(__ballot(!ok) == 0ull, 1)) {
+      const float y = 1.0f / den;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[c][e] = div_cr(d[c][e], den, y) + gb[c][e];
+    } else {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[c][e] = d[c][e] / den + gb[c][e];
     }
   }
   if (a.yout) {
@@ -80,11 +96,10 @@ __global__ __launch_bounds__(256) void k_rows(RowArgs a) {
     const int off = a.dst_off_dev ? *a.dst_off_dev + a.dst_off : a.dst_off;
     const long dst = (long)(r / a.rpb) * a.dst_bstride + off + (r % a.rpb);
     int8_t* qr = a.q + dst * a.ldq;
+    uint32_t qd[NCH];
+    quant_pack<4 * NCH>(&v[0][0], sc, qd);
 #pragma unroll
-    for (int c = 0; c < NCH; ++c)
-      *reinterpret_cast<uint32_t*>(qr + 4 * (lane + 64 * c)) =
-          pack4_i8(quant_val(v[c][0], sc), quant_val(v[c][1], sc), quant_val(v[c][2], sc),
-                   quant_val(v[c][3], sc));
+    for (int c = 0; c < NCH; ++c) *reinterpret_cast<uint32_t*>(qr + 4 * (lane + 64 * c)) = qd[c];
     if (lane == 0) a.s[dst] = sc;
   }
 }

@@ -128,8 +128,8 @@ class QtxModel:
                   _ptr(out), _stream())
         return out
 
-    def generator(self, x, want_logp: bool = True):
-        """x [M,512] -> (logp [M,V] or None, ids int64 [M])."""
+    def generator(self, x, want_logp: bool = True, return_logits: bool = False):
+        """x [M,512] -> (logp [M,V] or None, ids int64 [M]) (+ raw logits [M,V])."""
         torch = _torch()
         M = x.shape[0]
         V = self.cfg.tgt_vocab
@@ -138,6 +138,8 @@ class QtxModel:
         ws = torch.empty((M * V,), dtype=torch.float32, device=self.device)
         _lib.call("qtx_generator", self.handle, _ptr(x), M, _ptr(logp), _ptr(ids), _ptr(ws),
                   ws.numel() * 4, _stream())
+        if return_logits:
+            return logp, ids, ws.view(M, V)
         return logp, ids
 
 

@@ -72,13 +72,15 @@ def qexp(x):
 
 
 def _butterfly(v):
-    """xor-butterfly over the last axis (64 lanes): off = 32, 16, ..., 1; returns lane 0."""
+    """Balanced pairwise tree over the 64 lane values in natural order — an xor-butterfly
+    with offsets 1, 2, 4, ..., 32; returns lane 0.  The HIP side computes the same tree
+    with DPP (qtx_common.h:wave_sum)."""
     v = np.asarray(v, f32)
     lanes = np.arange(v.shape[-1])
-    off = v.shape[-1] // 2
-    while off >= 1:
+    off = 1
+    while off < v.shape[-1]:
         v = v + v[..., lanes ^ off]
-        off //= 2
+        off *= 2
     return v[..., 0]
 
 
@@ -342,14 +344,18 @@ class OracleModel:
         e = lut[ids] * f32(np.sqrt(512.0) if lut.shape[1] == 512 else np.sqrt(lut.shape[1]))
         return (e + self.pe[pos0:pos0 + ids.shape[1]][None]).astype(f32)
 
-    def generator(self, x):
-        """Generator.forward (generator.py:14-15) + first-index argmax
-        (reference/onnx_reference_inference.py:640-641).  Returns (logprobs, ids)."""
+    def logits(self, x):
+        """proj(x) of generator.py:15: sequential fma chain over k from 0, then + bias."""
         x = np.asarray(x, f32)
         acc = np.zeros((x.shape[0], self.gen_w.shape[0]), f32)
         for k in range(x.shape[1]):
             acc = fma32(x[:, k, None], self.gen_w[None, :, k], acc)
-        logits = acc + self.gen_b
+        return (acc + self.gen_b).astype(f32)
+
+    def generator(self, x):
+        """Generator.forward (generator.py:14-15) + first-index argmax
+        (reference/onnx_reference_inference.py:640-641).  Returns (logprobs, ids)."""
+        logits = self.logits(x)
         m = logits.max(axis=-1)
         z = logits - m[:, None]
         lse = np.log(row_sum_lanesplit(qexp(z))).astype(f32)

@@ -64,6 +64,26 @@ def test_greedy_decode_matches_oracle(torch, gpu_model, oracle_model, golden_mod
     np.testing.assert_array_equal(ys, ref)
 
 
+@pytest.mark.parametrize("env", [{"QTX_NO_GRAPH": "1"}, {"QTX_UNFUSED": "1"}])
+def test_greedy_paths_agree(torch, gpu_model, golden_model, monkeypatch, env):
+    """The fused+graph decode step, the fused eager step and the unfused kernels agree."""
+    from qtx.decode import greedy_decode
+    src, m = golden_model["src"], golden_model["src_mask"]
+    ref = greedy_decode(gpu_model, src, m, 40, 0)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    np.testing.assert_array_equal(greedy_decode(gpu_model, src, m, 40, 0), ref)
+
+
+def test_greedy_long_source_unfused_path(torch, gpu_model, oracle_model):
+    """Sources longer than the fused kernel's 128-key LDS budget take the unfused path."""
+    from qtx.decode import greedy_decode
+    rng = np.random.default_rng(9)
+    src, m = make_batch(rng, 2, 160, lens=[160, 100])
+    ys = greedy_decode(gpu_model, src, m, 10, 0)
+    np.testing.assert_array_equal(ys, oracle_model.greedy_decode(src, m, 10))
+
+
 def test_greedy_batch_invariance(torch, gpu_model):
     """Per-token quantization makes results batch-composition invariant:
     a sentence decoded inside a batch of 32 equals it decoded alone."""

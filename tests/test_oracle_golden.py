@@ -75,9 +75,14 @@ def test_attention_core(golden_ops):
 
 
 def test_embed_and_pe(golden_ops, oracle_model):
-    np.testing.assert_array_equal(oracle_model.pe[:128], golden_ops["pe_ref"])
-    np.testing.assert_array_equal(oracle_model.embed(golden_ops["emb_ids"], oracle_model.src_lut),
-                                  golden_ops["emb_ref"])
+    """positional_encodings.py:14-20 is torch float32 sin/cos on the host CPU, whose last
+    ulp varies across CPUs; on the fixture's host it is bit-identical."""
+    pe = oracle_model.pe[:128]
+    assert np.abs(pe - golden_ops["pe_ref"]).max() <= 1.2e-7
+    emb = oracle_model.embed(golden_ops["emb_ids"], oracle_model.src_lut)
+    if np.array_equal(pe, golden_ops["pe_ref"]):
+        np.testing.assert_array_equal(emb, golden_ops["emb_ref"])
+    assert np.abs(emb - golden_ops["emb_ref"]).max() < 1e-6
 
 
 def test_generator(golden_ops, oracle_model):
@@ -96,8 +101,8 @@ def test_qexp_accuracy():
 def test_encoder_module_statistical(golden_model, oracle_model):
     """End to end through 6 layers: most values agree tightly; rint near-tie flips
      perturb the rest.  Embedding input is bit-exact."""
-    np.testing.assert_array_equal(
-        oracle_model.embed(golden_model["src"], oracle_model.src_lut), golden_model["enc_in"])
+    assert np.abs(oracle_model.embed(golden_model["src"], oracle_model.src_lut)
+                  - golden_model["enc_in"]).max() < 1e-6
     mem = oracle_model.encode(golden_model["enc_in"], golden_model["src_mask"])
     d = np.abs(mem - golden_model["memory"])
     assert np.median(d) < 1e-3 and d.max() < 0.5
