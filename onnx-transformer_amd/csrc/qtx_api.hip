@@ -2,6 +2,7 @@
 // encoder / decoder / greedy-decode drivers built from the kernels of qtx_kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -73,12 +74,17 @@ struct DecLayer {
 };
 
 struct GraphKey {
-  int B, S, L;
+  int B, S, L, G;
   const void *ws, *ids, *mask;
   bool operator<(const GraphKey& o) const {
-    return std::tie(B, S, L, ws, ids, mask) < std::tie(o.B, o.S, o.L, o.ws, o.ids, o.mask);
+    return std::tie(B, S, L, G, ws, ids, mask) <
+           std::tie(o.B, o.S, o.L, o.G, o.ws, o.ids, o.mask);
   }
 };
+
+// The fused decode runs the batch as up to QTX_MAX_GROUPS independent sub-batches, each a
+// graph on its own stream (qtx_greedy_decode).
+constexpr int QTX_MAX_GROUPS = 4;
 
 struct qtx_model {
   qtx_config cfg;
@@ -92,11 +98,12 @@ struct qtx_model {
   size_t bytes = 0;
   // decode-step graphs, keyed by shape and the buffers baked into them
   std::mutex mu;
-  hipStream_t gstream = nullptr;
-  hipEvent_t ev_in = nullptr, ev_out = nullptr;
-  std::map<GraphKey, hipGraphExec_t> graphs;
+  hipStream_t gstream[QTX_MAX_GROUPS] = {};
+  hipEvent_t ev_in = nullptr, ev_out[QTX_MAX_GROUPS] = {};
+  std::map<GraphKey, std::vector<hipGraphExec_t>> graphs;   // one graph per sub-batch
   void clear_graphs() {
-    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto& kv : graphs)
+      for (hipGraphExec_t e : kv.second) (void)hipGraphExecDestroy(e);
     graphs.clear();
   }
 };
@@ -285,11 +292,14 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
 
 int32_t qtx_model_destroy(qtx_model* m) {
   if (!m) return QTX_OK;
-  if (m->gstream) (void)hipStreamSynchronize(m->gstream);
+  for (hipStream_t s : m->gstream)
+    if (s) (void)hipStreamSynchronize(s);
   m->clear_graphs();
   if (m->ev_in) (void)hipEventDestroy(m->ev_in);
-  if (m->ev_out) (void)hipEventDestroy(m->ev_out);
-  if (m->gstream) (void)hipStreamDestroy(m->gstream);
+  for (int i = 0; i < QTX_MAX_GROUPS; ++i) {
+    if (m->ev_out[i]) (void)hipEventDestroy(m->ev_out[i]);
+    if (m->gstream[i]) (void)hipStreamDestroy(m->gstream[i]);
+  }
   if (m->mem) (void)hipFree(m->mem);
   delete m;
   return QTX_OK;
@@ -513,7 +523,28 @@ struct GreedyWS {
   float* logits;
   int* step;          // [0] = decode position, [1] = argmax arrival counter
   unsigned* rowmax;   // [B] FFN1 row absmax (A_F32Q operand of FFN2)
+  // fused-decode sub-batches: step scratch (grp[0] = dec) and step counters, 4 ints each
+  std::vector<Scratch> grp;
+  int* gsteps;
 };
+
+// Sub-batch split of the fused decode.  Sentences are independent (per-token quantization:
+// no value depends on another sentence), and one sub-batch's step is a chain of ~75
+// latency-bound kernels that each occupy a fraction of the 256 CUs, so G sub-batches on
+// G streams overlap almost perfectly.  QTX_DECODE_GROUPS overrides the default.
+struct Groups {
+  int G, Bg;   // G groups of Bg rows (the last one may be shorter)
+  int b0(int i) const { return i * Bg; }
+  int rows(int i, int B) const { return std::min(B, (i + 1) * Bg) - i * Bg; }
+};
+Groups decode_groups(int B) {
+  int G = 1;   // measured: concurrent sub-batch graphs on extra HW queues run slower
+  if (const char* v = getenv("QTX_DECODE_GROUPS"))
+    if (*v) G = atoi(v);
+  G = std::max(1, std::min(std::min(G, QTX_MAX_GROUPS), B));
+  const int Bg = (B + G - 1) / G;
+  return Groups{(B + Bg - 1) / Bg, Bg};   // no empty group
+}
 
 GreedyWS carve_greedy(Arena& ar, const qtx_config& c, int B, int S, int max_len) {
   GreedyWS g;
@@ -532,7 +563,29 @@ GreedyWS carve_greedy(Arena& ar, const qtx_config& c, int B, int S, int max_len)
   g.logits = ar.take<float>((size_t)B * c.tgt_vocab);
   g.step = ar.take<int>(4);
   g.rowmax = ar.take<unsigned>((size_t)B);
+  const Groups gr = decode_groups(B);
+  g.grp.push_back(g.dec);
+  for (int i = 1; i < gr.G; ++i) g.grp.push_back(carve_scratch(ar, c, gr.Bg));
+  g.gsteps = ar.take<int>(4 * QTX_MAX_GROUPS);
   return g;
+}
+
+// The workspace of sub-batch i (rows b0 ..): every per-sentence buffer offset by b0.
+GreedyWS group_view(const GreedyWS& g, const qtx_config& c, int i, int b0, int S,
+                    int max_len) {
+  const long D = c.d_model;
+  GreedyWS v = g;
+  v.dec = g.grp[i];
+  for (int l = 0; l < c.n_layers; ++l) {
+    v.kc[l] += b0 * max_len * D; v.vc[l] += b0 * max_len * D;
+    v.skc[l] += b0 * max_len; v.svc[l] += b0 * max_len;
+    v.cross.k8[l] += b0 * S * D; v.cross.v8[l] += b0 * S * D;
+    v.cross.sk[l] += b0 * S; v.cross.sv[l] += b0 * S;
+  }
+  v.logits += (long)b0 * c.tgt_vocab;
+  v.rowmax += b0;
+  v.step = g.gsteps + 4 * i;
+  return v;
 }
 
 bool env_flag(const char* name);
@@ -556,57 +609,80 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
   const bool ffn_rowmax = env_flag("QTX_FFN_ROWMAX");
   const bool fused_ln = env_flag("QTX_FUSED_LN");
   Scratch& s = g.dec;
+  // Timing experiments only (wrong results): QTX_ABLATE=<bitmask> drops kernel classes
+  // from the step (replaced by an empty kernel with QTX_ABLATE_NOP=1) to measure what
+  // each costs inside the real graph.  1 LN, 2 QKV/Qc, 4 self-attn, 8 cross-attn,
+  // 16 O/Oc, 32 FFN1, 64 h-quant, 128 FFN2, 256 tail.
+  const char* abl_env = getenv("QTX_ABLATE");
+  const int abl = abl_env ? (int)strtol(abl_env, nullptr, 0) : 0;
+  const bool abl_nop = env_flag("QTX_ABLATE_NOP");
+#define QTX_RUN(bit, launch)                   \
+  do {                                         \
+    if (abl & (bit)) {                         \
+      if (abl_nop) HIPCHK(launch_nop(st));     \
+    } else {                                   \
+      HIPCHK(launch);                          \
+    }                                          \
+  } while (0)
   // out = epilogue(quant(LN(x)) . W^T): LayerNorm + per-token quant as its own kernel
   // (one wave per row, 2.7 us) then the int8 GEMM — measured faster than recomputing the
   // LayerNorm of all rows in every GEMM workgroup (the A_LN prologue, QTX_FUSED_LN=1).
+#define QTX_RUNRC(bit, expr)                   \
+  do {                                         \
+    if (abl & (bit)) {                         \
+      if (abl_nop) HIPCHK(launch_nop(st));     \
+    } else {                                   \
+      RC(expr);                                \
+    }                                          \
+  } while (0)
   auto ln_linear = [&](const QLin& W, const float* const* ln, int flags, float* out,
-                       long ldo) -> int {
+                       long ldo, int bit) -> int {
     SkinnyArgs k = skinny(wb, W, B, fused_ln ? A_LN : A_I8, flags, out, ldo);
     if (fused_ln) {
       k.X = s.x; k.ldx = D; k.ln_a = ln[0]; k.ln_b = ln[1];
     } else {
-      RC(ln_quant(s.x, B, ln, D, s.a8, s.sa, st));
+      QTX_RUNRC(1, ln_quant(s.x, B, ln, D, s.a8, s.sa, st));
       k.A = s.a8; k.sa = s.sa;
     }
-    HIPCHK(launch_skinny(k, wb, st));
+    QTX_RUN(bit, launch_skinny(k, wb, st));
     return QTX_OK;
   };
   for (int l = 0; l < c.n_layers; ++l) {
     const DecLayer& L = m->dec[l];
     SkinnyArgs a;
-    RC(ln_linear(L.qkv, L.ln[0], 0, s.y, 3 * D));
+    RC(ln_linear(L.qkv, L.ln[0], 0, s.y, 3 * D, 2));
     DecAttnArgs at{};
     at.y = s.y; at.ldy = 3 * D; at.kv_new = 1; at.step = g.step;
     at.kc = g.kc[l]; at.vc = g.vc[l]; at.skc = g.skc[l]; at.svc = g.svc[l]; at.kv_bs = max_len;
     at.a8 = s.a8; at.sa = s.sa;
-    HIPCHK(launch_dec_attn(at, B, st));
+    QTX_RUN(4, launch_dec_attn(at, B, st));
     a = skinny(wb, L.o, B, A_I8, EPI_RESIDUAL, s.x, D);
     a.A = s.a8; a.sa = s.sa; a.res = s.x; a.ldr = D;
-    HIPCHK(launch_skinny(a, wb, st));
-    RC(ln_linear(L.cq, L.ln[1], 0, s.y, D));
+    QTX_RUN(16, launch_skinny(a, wb, st));
+    RC(ln_linear(L.cq, L.ln[1], 0, s.y, D, 2));
     at = DecAttnArgs{};
     at.y = s.y; at.ldy = D; at.kv_new = 0; at.S = S; at.mask = src_mask;
     at.kc = g.cross.k8[l]; at.vc = g.cross.v8[l]; at.skc = g.cross.sk[l];
     at.svc = g.cross.sv[l]; at.kv_bs = S;
     at.a8 = s.a8; at.sa = s.sa;
-    HIPCHK(launch_dec_attn(at, B, st));
+    QTX_RUN(8, launch_dec_attn(at, B, st));
     a = skinny(wb, L.co, B, A_I8, EPI_RESIDUAL, s.x, D);
     a.A = s.a8; a.sa = s.sa; a.res = s.x; a.ldr = D;
     a.zero = g.rowmax; a.zero_n = B;
-    HIPCHK(launch_skinny(a, wb, st));
+    QTX_RUN(16, launch_skinny(a, wb, st));
     if (ffn_rowmax) {   // FFN2 quantizes h itself from FFN1's atomic row maxima
       a = skinny(wb, L.w1, B, A_LN, EPI_RELU | EPI_ROWMAX, s.y, F);
       a.X = s.x; a.ldx = D; a.ln_a = L.ln[2][0]; a.ln_b = L.ln[2][1]; a.rowmax_out = g.rowmax;
-      HIPCHK(launch_skinny(a, wb, st));
+      QTX_RUN(32, launch_skinny(a, wb, st));
       a = skinny(wb, L.w2, B, A_F32Q, EPI_RESIDUAL, s.x, D);
       a.X = s.y; a.ldx = F; a.rowmax_in = g.rowmax; a.res = s.x; a.ldr = D;
-      HIPCHK(launch_skinny(a, wb, st));
+      QTX_RUN(128, launch_skinny(a, wb, st));
     } else {            // one wave per row quantizes h (quant_linear.py:30-43), then FFN2
-      RC(ln_linear(L.w1, L.ln[2], EPI_RELU, s.y, F));
-      RC(quant(s.y, F, B, F, s.a8, s.sa, st));
+      RC(ln_linear(L.w1, L.ln[2], EPI_RELU, s.y, F, 32));
+      QTX_RUNRC(64, quant(s.y, F, B, F, s.a8, s.sa, st));
       a = skinny(wb, L.w2, B, A_I8, EPI_RESIDUAL, s.x, D);
       a.A = s.a8; a.sa = s.sa; a.res = s.x; a.ldr = D;
-      HIPCHK(launch_skinny(a, wb, st));
+      QTX_RUN(128, launch_skinny(a, wb, st));
     }
   }
   if (getenv("QTX_DBG_TAIL")) {   // bisection aid: reference-shaped tail kernels
@@ -619,12 +695,14 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
                         c.max_len, s.x, D, st));
     return QTX_OK;
   }
-  HIPCHK(launch_generator_mfma(s.x, D, B, m->dec_norm[0], m->dec_norm[1], m->gen_wt, m->gen_b,
-                               c.tgt_vocab, g.logits, st));
-  HIPCHK(launch_argmax_embed(g.logits, B, c.tgt_vocab, ids, max_len, g.step,
-                             reinterpret_cast<unsigned*>(g.step + 1), m->tgt_lut, m->pe,
-                             c.max_len, s.x, st));
+  QTX_RUN(256, launch_generator_mfma(s.x, D, B, m->dec_norm[0], m->dec_norm[1], m->gen_wt,
+                                     m->gen_b, c.tgt_vocab, g.logits, st));
+  QTX_RUN(256, launch_argmax_embed(g.logits, B, c.tgt_vocab, ids, max_len, g.step,
+                                   reinterpret_cast<unsigned*>(g.step + 1), m->tgt_lut, m->pe,
+                                   c.max_len, s.x, st));
   return QTX_OK;
+#undef QTX_RUN
+#undef QTX_RUNRC
 }
 
 // The reference-shaped unfused step (any key count up to 512).
@@ -781,47 +859,103 @@ int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t*
     for (int t = 0; t + 1 < max_len; ++t) RC(greedy_step_unfused(m, g, B, S, max_len, ids, src_mask, st));
     return QTX_OK;
   }
-  // first decoder input: tgt_embed(ys[:, 0]) at position 0; later ones come from the
-  // argmax kernel of the previous step
-  HIPCHK(launch_embed(ids, max_len, B, 1, g.step, 0, m->tgt_lut, c.tgt_vocab, m->pe,
-                      c.max_len, g.dec.x, D, st));
+  // sub-batches: each has its own step scratch and step counter; the first decoder input
+  // is tgt_embed(ys[:, 0]) at position 0, later ones come from the previous step's argmax
+  const Groups gr = decode_groups(B);
+  std::vector<GreedyWS> gv;
+  HIPCHK(hipMemsetAsync(g.gsteps, 0, sizeof(int) * 4 * QTX_MAX_GROUPS, st));
+  for (int i = 0; i < gr.G; ++i) {
+    gv.push_back(group_view(g, c, i, gr.b0(i), S, max_len));
+    HIPCHK(launch_embed(ids + (long)gr.b0(i) * max_len, max_len, gr.rows(i, B), 1, gv[i].step,
+                        0, m->tgt_lut, c.tgt_vocab, m->pe, c.max_len, gv[i].dec.x, D, st));
+  }
+  auto step_fn = [&](int i, hipStream_t s) {
+    return greedy_step_fused(m, gv[i], gr.rows(i, B), S, max_len, ids + (long)gr.b0(i) * max_len,
+                             src_mask + (long)gr.b0(i) * S, s);
+  };
   if (env_flag("QTX_NO_GRAPH")) {
-    for (int t = 0; t + 1 < max_len; ++t) RC(greedy_step_fused(m, g, B, S, max_len, ids, src_mask, st));
+    for (int t = 0; t + 1 < max_len; ++t)
+      for (int i = 0; i < gr.G; ++i) RC(step_fn(i, st));
     return QTX_OK;
   }
-  // One decode step captured once per (shape, buffers) as a hipGraph and replayed
-  // max_len-1 times on the model's stream, ordered after / before the caller's stream.
+  // One decode step per sub-batch captured once per (shape, buffers) as a hipGraph on its
+  // own stream and replayed max_len-1 times there; the streams fork from and join back
+  // into the caller's stream.
   qtx_model* mm = const_cast<qtx_model*>(m);
   std::lock_guard<std::mutex> lock(mm->mu);
-  if (!mm->gstream) {
-    HIPCHK(hipStreamCreateWithFlags(&mm->gstream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&mm->ev_in, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&mm->ev_out, hipEventDisableTiming));
-  }
-  const GraphKey key{B, S, max_len, ws, ids, src_mask};
+  if (!mm->ev_in) HIPCHK(hipEventCreateWithFlags(&mm->ev_in, hipEventDisableTiming));
+  for (int i = 0; i < gr.G; ++i)
+    if (!mm->gstream[i]) {
+      HIPCHK(hipStreamCreateWithFlags(&mm->gstream[i], hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&mm->ev_out[i], hipEventDisableTiming));
+    }
+  // steps per graph: the whole decode in one graph by default (one graph launch); must
+  // divide max_len-1 (the step position is read from device memory, so replays chain)
+  int per_graph = max_len - 1;
+  if (const char* v = getenv("QTX_GRAPH_STEPS"))
+    if (*v && atoi(v) > 0 && (max_len - 1) % atoi(v) == 0) per_graph = atoi(v);
+  if (max_len <= 1) return QTX_OK;
+  const GraphKey key{B, S, max_len, gr.G * 1000 + per_graph, ws, ids, src_mask};
   auto it = mm->graphs.find(key);
   if (it == mm->graphs.end()) {
     if (mm->graphs.size() >= 16) mm->clear_graphs();
-    hipGraph_t graph = nullptr;
-    HIPCHK(hipStreamBeginCapture(mm->gstream, hipStreamCaptureModeThreadLocal));
-    const int rc = greedy_step_fused(m, g, B, S, max_len, ids, src_mask, mm->gstream);
-    const hipError_t ec = hipStreamEndCapture(mm->gstream, &graph);
-    if (rc != QTX_OK) {
-      if (graph) (void)hipGraphDestroy(graph);
-      return rc;
+    std::vector<hipGraphExec_t> execs;
+    auto drop = [&] {
+      for (hipGraphExec_t e : execs) (void)hipGraphExecDestroy(e);
+    };
+    for (int i = 0; i < gr.G; ++i) {
+      hipGraph_t graph = nullptr;
+      hipError_t e = hipStreamBeginCapture(mm->gstream[i], hipStreamCaptureModeThreadLocal);
+      if (e != hipSuccess) { drop(); HIPCHK(e); }
+      int rc = QTX_OK;
+      for (int t = 0; t < per_graph && rc == QTX_OK; ++t) rc = step_fn(i, mm->gstream[i]);
+      e = hipStreamEndCapture(mm->gstream[i], &graph);
+      if (rc != QTX_OK || e != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        drop();
+        if (rc != QTX_OK) return rc;
+        HIPCHK(e);
+      }
+      hipGraphExec_t exec = nullptr;
+      e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      if (e != hipSuccess) { drop(); HIPCHK(e); }
+      execs.push_back(exec);
     }
-    HIPCHK(ec);
-    hipGraphExec_t exec = nullptr;
-    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    HIPCHK(ei);
-    it = mm->graphs.emplace(key, exec).first;
+    it = mm->graphs.emplace(key, std::move(execs)).first;
   }
-  HIPCHK(hipEventRecord(mm->ev_in, st));
-  HIPCHK(hipStreamWaitEvent(mm->gstream, mm->ev_in, 0));
-  for (int t = 0; t + 1 < max_len; ++t) HIPCHK(hipGraphLaunch(it->second, mm->gstream));
-  HIPCHK(hipEventRecord(mm->ev_out, mm->gstream));
-  HIPCHK(hipStreamWaitEvent(st, mm->ev_out, 0));
+  // One sub-batch: replay on the caller's stream itself (a graph captured on one stream can
+  // be launched on any).  Several: fork to the model's streams and join back.
+  const bool fork = gr.G > 1;
+  hipStream_t ls[QTX_MAX_GROUPS];
+  for (int i = 0; i < gr.G; ++i) ls[i] = fork ? mm->gstream[i] : st;
+  if (fork) {
+    HIPCHK(hipEventRecord(mm->ev_in, st));
+    for (int i = 0; i < gr.G; ++i) HIPCHK(hipStreamWaitEvent(ls[i], mm->ev_in, 0));
+  }
+  hipEvent_t tg0 = nullptr, tg1 = nullptr;   // QTX_TIME_GRAPH: diagnostic timing to stderr
+  const bool time_graph = env_flag("QTX_TIME_GRAPH");
+  if (time_graph) {
+    HIPCHK(hipEventCreate(&tg0));
+    HIPCHK(hipEventCreate(&tg1));
+    HIPCHK(hipEventRecord(tg0, ls[0]));
+  }
+  for (int t = 0; t < (max_len - 1) / per_graph; ++t)
+    for (int i = 0; i < gr.G; ++i) HIPCHK(hipGraphLaunch(it->second[i], ls[i]));
+  if (time_graph) {
+    float ms = 0.0f;
+    HIPCHK(hipEventRecord(tg1, ls[0]));
+    HIPCHK(hipEventSynchronize(tg1));
+    HIPCHK(hipEventElapsedTime(&ms, tg0, tg1));
+    fprintf(stderr, "qtx: decode graphs %.3f ms (%d steps, group 0)\n", ms, max_len - 1);
+    (void)hipEventDestroy(tg0);
+    (void)hipEventDestroy(tg1);
+  }
+  if (fork)
+    for (int i = 0; i < gr.G; ++i) {
+      HIPCHK(hipEventRecord(mm->ev_out[i], ls[i]));
+      HIPCHK(hipStreamWaitEvent(st, mm->ev_out[i], 0));
+    }
   return QTX_OK;
 }
 

@@ -13,6 +13,22 @@
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
+// In-kernel phase stamps for diagnosis (tools/kernel_bench.py --stamps): compiled in only
+// with -DQTX_STAMPS; thread 0 of each block records s_memtime at phase boundaries into
+// qtx_stamp_buf[block][slot] (a device buffer of its own; never read by the kernels).
+#ifdef QTX_STAMPS
+#define QTX_STAMP(slot)                                                                 \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && qtx_stamp_buf)                                                \
+      qtx_stamp_buf[(blockIdx.y * gridDim.x + blockIdx.x) * 16 + (slot)] =                \
+          __builtin_amdgcn_s_memtime();                                                   \
+  } while (0)
+#else
+#define QTX_STAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
+
 namespace qtx {
 
 // ---------------------------------------------------------------- wave reductions
@@ -82,9 +98,23 @@ __device__ __forceinline__ bool div_ok(float a) {
   const float m = fabsf(a);
   return m == 0.0f || (m > 0x1p-60f && m < 0x1p60f);
 }
+// The same guard folded over many numerators without branches: track max(|a|) and
+// min(|a| - 1) on the bit patterns (|a| = 0 wraps to UINT_MAX and drops out of the min),
+// then test once.  ok() == AND of div_ok(a) over everything added.
+struct DivRange {
+  uint32_t mn = 0xffffffffu, mx = 0u;
+  __device__ __forceinline__ void add(float a) {
+    const uint32_t m = __float_as_uint(a) & 0x7fffffffu;
+    mx = max(mx, m);
+    mn = min(mn, m - 1u);
+  }
+  __device__ __forceinline__ bool ok() const {
+    return mx < 0x5d800000u && mn >= 0x21800000u;   // |a| < 2^60, |a| > 2^-60
+  }
+};
 __device__ __forceinline__ bool divisor_ok(float b) {
-  const float m = fabsf(b);
-  return m > 0x1p-30f && m < 0x1p30f;
+  const uint32_t m = __float_as_uint(b) & 0x7fffffffu;
+  return m - 0x30800001u < 0x4e800000u - 0x30800001u;   // 2^-30 < |b| < 2^30
 }
 
 // ---------------------------------------------------------------- quantizer

@@ -14,6 +14,13 @@
 #include "qtx_common.h"
 #include "qtx_kernels.h"
 
+#ifdef QTX_STAMPS
+__device__ unsigned long long* qtx_stamp_buf;
+extern "C" int qtx_debug_set_stamps(void* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(qtx_stamp_buf), &buf, sizeof(buf));
+}
+#endif
+
 namespace qtx {
 
 __device__ __forceinline__ uint4 unpack_i4(uint2 h) {
@@ -73,18 +80,20 @@ __device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float* a, 
     ga[c][0] = ta.x; ga[c][1] = ta.y; ga[c][2] = ta.z; ga[c][3] = ta.w;
     gb[c][0] = tb.x; gb[c][1] = tb.y; gb[c][2] = tb.z; gb[c][3] = tb.w;
   }
-  bool ok = true;
+  DivRange rg;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
-    ok &= divisor_ok(den[j]);
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         v[j][c][e] = ga[c][e] * v[j][c][e];     // numerator a * d
-        ok &= div_ok(v[j][c][e]);
+        rg.add(v[j][c][e]);
       }
   }
+  bool ok = rg.ok();
+#pragma unroll
+  for (int j = 0; j < R; ++j) ok &= divisor_ok(den[j]);
   if (__builtin_expect(__ballot(!ok) == 0ull, 1)) {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -126,7 +135,7 @@ __device__ __forceinline__ void quant_rows512(const float (&v)[R][2][4], uint32_
 // =====================================================================================
 // k_skinny
 // =====================================================================================
-template <int MF, int K, int WBITS>
+template <int MF, int K, int WBITS, int AMODE, int FLAGS>
 __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
   constexpr int BM = 16 * MF;
   constexpr int KW = K / 4;       // K range of one wave
@@ -140,6 +149,7 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
   const int fr = lane & 15, fg = lane >> 4;
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * BM;
 
+  QTX_STAMP(0);
   if (g.zero && blockIdx.x == 0 && blockIdx.y == 0)
     for (int i = tid; i < g.zero_n; i += 256) g.zero[i] = 0u;
 
@@ -160,7 +170,7 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
   const int col = n0 + fr;
   const bool cok = col < g.N;
   float swc = 0.0f, bc = 0.0f, rv[MF][4];
-  const bool resid = g.flags & EPI_RESIDUAL;
+  constexpr bool resid = FLAGS & EPI_RESIDUAL;
   if (wave == 0) {
     swc = cok ? g.sw[col] : 0.0f;
     bc = cok ? g.bias[col] : 0.0f;
@@ -176,7 +186,7 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
   // 2. A panel (int8) and per-row scales into LDS.  Every branch issues all of its
   //    global loads before consuming any (one memory latency, not one per row).
   constexpr int RPW = BM / 4;  // rows per wave: r = wave + 4*j
-  if (g.amode == A_I8) {
+  if constexpr (AMODE == A_I8) {
     constexpr int CPR = K / 16, NLD = BM * CPR / 256;
     uint4 v[NLD];
 #pragma unroll
@@ -191,7 +201,7 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
       *reinterpret_cast<uint4*>(As + r * LDA + 16 * (idx % CPR)) =
           (m0 + r < g.M) ? v[j] : make_uint4(0, 0, 0, 0);
     }
-  } else if (g.amode == A_LN) {
+  } else if constexpr (AMODE == A_LN) {
     float v[RPW][2][4];
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
@@ -250,6 +260,7 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
   }
   __syncthreads();
 
+  QTX_STAMP(1);
   // 3. MFMA over this wave's K range
   v4i acc[MF];
 #pragma unroll
@@ -276,13 +287,14 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
     for (int i = 0; i < MF; ++i) red[wave - 1][i][lane] = acc[i];
   __syncthreads();
   if (wave != 0) return;
+  QTX_STAMP(2);
 #pragma unroll
   for (int w = 0; w < 3; ++w)
 #pragma unroll
     for (int i = 0; i < MF; ++i) acc[i] += red[w][i][lane];
 
   // 5. epilogue (C layout: col = lane & 15, row = 4*(lane>>4) + e)
-  const bool relu = g.flags & EPI_RELU, rmax = g.flags & EPI_ROWMAX;
+  constexpr bool relu = FLAGS & EPI_RELU, rmax = FLAGS & EPI_ROWMAX;
 #pragma unroll
   for (int i = 0; i < MF; ++i) {
 #pragma unroll
@@ -290,10 +302,10 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
       const int r = 16 * i + 4 * fg + e, row = m0 + r;
       const bool ok = cok && row < g.M;
       float y = ((float)acc[i][e] * sas[r]) * swc + bc;
-      if (relu) y = y > 0.0f ? y : 0.0f;
-      if (resid) y = rv[i][e] + y;
+      if constexpr (relu) y = y > 0.0f ? y : 0.0f;
+      if constexpr (resid) y = rv[i][e] + y;
       if (ok) g.out[(long)row * g.ldo + col] = y;
-      if (rmax) {
+      if constexpr (rmax) {
         float am = ok ? fabsf(y) : 0.0f;
         am = fmaxf(am, __shfl_xor(am, 8, 64));
         am = fmaxf(am, __shfl_xor(am, 4, 64));
@@ -303,26 +315,45 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
       }
     }
   }
+  QTX_STAMP(3);
+}
+
+// dispatch: the prologue mode and epilogue flags are template parameters (no runtime
+// branches per output element).  Supported: K 512 with A_I8 / A_LN, K 2048 with A_I8 /
+// A_F32Q; flags 0, RELU, RESIDUAL, RELU|ROWMAX.
+template <int MF, int K, int WB, int AM>
+hipError_t skinny_flags(const SkinnyArgs& g, dim3 grid, hipStream_t st) {
+  switch (g.flags) {
+    case 0: k_skinny<MF, K, WB, AM, 0><<<grid, 256, 0, st>>>(g); break;
+    case EPI_RELU: k_skinny<MF, K, WB, AM, EPI_RELU><<<grid, 256, 0, st>>>(g); break;
+    case EPI_RESIDUAL: k_skinny<MF, K, WB, AM, EPI_RESIDUAL><<<grid, 256, 0, st>>>(g); break;
+    case EPI_RELU | EPI_ROWMAX:
+      k_skinny<MF, K, WB, AM, EPI_RELU | EPI_ROWMAX><<<grid, 256, 0, st>>>(g);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+template <int MF, int WB>
+hipError_t skinny_mode(const SkinnyArgs& g, dim3 grid, hipStream_t st) {
+  if (g.K == 512) {
+    if (g.amode == A_I8) return skinny_flags<MF, 512, WB, A_I8>(g, grid, st);
+    if (g.amode == A_LN) return skinny_flags<MF, 512, WB, A_LN>(g, grid, st);
+  } else if (g.K == 2048) {
+    if (g.amode == A_I8) return skinny_flags<MF, 2048, WB, A_I8>(g, grid, st);
+    if (g.amode == A_F32Q) return skinny_flags<MF, 2048, WB, A_F32Q>(g, grid, st);
+  }
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_skinny(const SkinnyArgs& g, int wbits, hipStream_t st) {
   if (g.M <= 0) return hipSuccess;
-  if (g.N % 16 || (g.K != 512 && g.K != 2048) || (g.amode == A_LN && g.K != 512))
-    return hipErrorInvalidValue;
+  if (g.N % 16) return hipErrorInvalidValue;
   const int MF = g.M <= 16 ? 1 : 2;
-  const dim3 grid(g.N / 16, (g.M + 16 * MF - 1) / (16 * MF)), block(256);
-#define QTX_SK(mf, k, wb) k_skinny<mf, k, wb><<<grid, block, 0, st>>>(g)
-  if (wbits == 8) {
-    if (MF == 1) { if (g.K == 512) QTX_SK(1, 512, 8); else QTX_SK(1, 2048, 8); }
-    else         { if (g.K == 512) QTX_SK(2, 512, 8); else QTX_SK(2, 2048, 8); }
-  } else if (wbits == 4) {
-    if (MF == 1) { if (g.K == 512) QTX_SK(1, 512, 4); else QTX_SK(1, 2048, 4); }
-    else         { if (g.K == 512) QTX_SK(2, 512, 4); else QTX_SK(2, 2048, 4); }
-  } else {
-    return hipErrorInvalidValue;
-  }
-#undef QTX_SK
-  return hipGetLastError();
+  const dim3 grid(g.N / 16, (g.M + 16 * MF - 1) / (16 * MF));
+  if (wbits == 8) return MF == 1 ? skinny_mode<1, 8>(g, grid, st) : skinny_mode<2, 8>(g, grid, st);
+  if (wbits == 4) return MF == 1 ? skinny_mode<1, 4>(g, grid, st) : skinny_mode<2, 4>(g, grid, st);
+  return hipErrorInvalidValue;
 }
 
 // =====================================================================================
@@ -343,6 +374,7 @@ __device__ __forceinline__ float block_max512(float v, float* scratch) {
   return m;
 }
 
+template <bool KV_NEW>
 __global__ __launch_bounds__(512) void k_dec_attn(DecAttnArgs a) {
   __shared__ uint32_t Ks[8][DEC_MAXK * 17];     // per head: key rows of 64 int8 (+4 B pad)
   __shared__ __attribute__((aligned(16))) uint8_t Vs[DEC_MAXK * 512];
@@ -351,29 +383,39 @@ __global__ __launch_bounds__(512) void k_dec_attn(DecAttnArgs a) {
   __shared__ float red[3][8];
   __shared__ __attribute__((aligned(16))) int8_t qrow[512];   // read back as dwords
   const int b = blockIdx.x, t = threadIdx.x, h = t >> 6, lane = t & 63;
+  QTX_STAMP(0);
   const float* yr = a.y + (long)b * a.ldy;
-  const int step = a.kv_new ? *a.step : 0;
-  const int Sk = a.kv_new ? step + 1 : a.S;
+  const int step = KV_NEW ? *a.step : 0;
+  const int Sk = KV_NEW ? step + 1 : a.S;
 
   // phase 0: issue the loads of the cached keys/values first (one memory latency):
   // row j = 32 uint4 of K and of V; thread t takes uint4 index t + 512*i
-  const int nk = a.kv_new ? step : a.S;
+  const int nk = KV_NEW ? step : a.S;
   const uint4* kb4 = reinterpret_cast<const uint4*>(a.kc + (long)b * a.kv_bs * 512);
   const uint4* vb4 = reinterpret_cast<const uint4*>(a.vc + (long)b * a.kv_bs * 512);
   constexpr int NLD = DEC_MAXK * 32 / 512;
+  // Loads sit behind a wave-uniform bound on the iteration and read a clamped index (row
+  // 0 always exists): a load under a divergent branch makes the compiler wait for it
+  // before the join, serializing them; unconditional clamped loads waste L1 bandwidth.
+  const int lastk = nk * 32 > 0 ? nk * 32 - 1 : 0;
+  const int nit = (nk * 32 + 511) >> 9;
   uint4 kr[NLD], vr[NLD];
 #pragma unroll
   for (int i = 0; i < NLD; ++i) {
-    const int idx = t + 512 * i;
-    if (idx < nk * 32) { kr[i] = kb4[idx]; vr[i] = vb4[idx]; }
+    if (i < nit) {
+      const int idx = min(t + 512 * i, lastk);
+      kr[i] = kb4[idx];
+      vr[i] = vb4[idx];
+    }
   }
-  const float skj = t < nk ? a.skc[(long)b * a.kv_bs + t] : 0.0f;
-  const float svj = t < nk ? a.svc[(long)b * a.kv_bs + t] : 0.0f;
+  const int tj = min(t, nk > 0 ? nk - 1 : 0);
+  const float skj = a.skc[(long)b * a.kv_bs + tj];
+  const float svj = a.svc[(long)b * a.kv_bs + tj];
 
   // phase 1: per-token quantization of the new q (and k, v) rows: one block reduction
   // for the three row maxima
   const float vq = yr[t];
-  const float vk = a.kv_new ? yr[512 + t] : 0.0f, vv = a.kv_new ? yr[1024 + t] : 0.0f;
+  const float vk = KV_NEW ? yr[512 + t] : 0.0f, vv = KV_NEW ? yr[1024 + t] : 0.0f;
   {
     const float wq = wave_max(fabsf(vq)), wk = wave_max(fabsf(vk)), wv = wave_max(fabsf(vv));
     if (lane == 0) { red[0][h] = wq; red[1][h] = wk; red[2][h] = wv; }
@@ -386,7 +428,7 @@ __global__ __launch_bounds__(512) void k_dec_attn(DecAttnArgs a) {
   }
   const float sq = quant_scale(amq, 127.0f);
   qrow[t] = (int8_t)quant_one(vq, sq);
-  if (a.kv_new) {
+  if constexpr (KV_NEW) {
     const float sk = quant_scale(amk, 127.0f), sv = quant_scale(amv, 127.0f);
     const int8_t qk = (int8_t)quant_one(vk, sk), qv = (int8_t)quant_one(vv, sv);
     const long row = (long)b * a.kv_bs + step;
@@ -412,13 +454,14 @@ __global__ __launch_bounds__(512) void k_dec_attn(DecAttnArgs a) {
   }
   if (t < nk) { sks[t] = skj; svs[t] = svj; }
   __syncthreads();
+  QTX_STAMP(1);
 
   // phase 3: head h
   uint32_t qd[16];
 #pragma unroll
   for (int w = 0; w < 16; ++w) qd[w] = reinterpret_cast<const uint32_t*>(qrow + h * 64)[w];
   float* P = Pb[h];
-  const uint8_t* mk = a.kv_new ? nullptr : a.mask + (long)b * a.S;
+  const uint8_t* mk = KV_NEW ? nullptr : a.mask + (long)b * a.S;
   float lmax = -3.0e38f;
   for (int j = lane; j < Sk; j += 64) {
     int acc = 0;
@@ -439,21 +482,25 @@ __global__ __launch_bounds__(512) void k_dec_attn(DecAttnArgs a) {
   const float den = wave_sum(lsum);
   for (int j = lane; j < Sk; j += 64) P[j] = rintf((P[j] / den) * 127.0f) / 127.0f;
   __builtin_amdgcn_wave_barrier();
+  QTX_STAMP(2);
   float acc = 0.0f;
 #pragma unroll 8
   for (int j = 0; j < Sk; ++j)
     acc = fmaf(P[j], (float)(int8_t)Vs[j * 512 + t] * svs[j], acc);
+  QTX_STAMP(3);
 
   // phase 4: quantize the context row (all heads) per token -> next GEMM's A operand
   const float sc = quant_scale(block_max512(fabsf(acc), red[0]), 127.0f);
   a.a8[(long)b * 512 + t] = (int8_t)quant_one(acc, sc);
   if (t == 0) a.sa[b] = sc;
+  QTX_STAMP(4);
 }
 
 hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st) {
   if (B <= 0) return hipSuccess;
   if (!a.kv_new && (a.S <= 0 || a.S > DEC_MAXK)) return hipErrorInvalidValue;
-  k_dec_attn<<<dim3(B), dim3(512), 0, st>>>(a);
+  if (a.kv_new) k_dec_attn<true><<<dim3(B), dim3(512), 0, st>>>(a);
+  else k_dec_attn<false><<<dim3(B), dim3(512), 0, st>>>(a);
   return hipGetLastError();
 }
 

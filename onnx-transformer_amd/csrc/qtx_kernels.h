@@ -123,6 +123,7 @@ hipError_t launch_pack_int4(const int8_t* q, int N, int K, uint8_t* packed, hipS
 hipError_t launch_u8_from_any(const void* src, int elem_bytes, long n, uint8_t* dst,
                               hipStream_t st);
 hipError_t launch_step_inc(int* step, hipStream_t st);
+hipError_t launch_nop(hipStream_t st);
 hipError_t launch_fill_col(int64_t* ids, long bs, int B, int64_t val, hipStream_t st);
 
 }  // namespace qtx

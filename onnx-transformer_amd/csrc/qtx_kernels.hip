@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void k_rows(RowArgs a) {
     const float var = wave_sum(ss) / (D - 1.0f);
     const float den = sqrtf(var) + 1e-6f;
     float gb[NCH][4];
-    bool ok = divisor_ok(den);
+    DivRange rg;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const float4 ga = *reinterpret_cast<const float4*>(a.ln_a + 4 * (lane + 64 * c));
@@ -62,8 +62,9 @@ __global__ __launch_bounds__(256) void k_rows(RowArgs a) {
       d[c][2] = ga.z * d[c][2]; d[c][3] = ga.w * d[c][3];
       gb[c][0] = tb.x; gb[c][1] = tb.y; gb[c][2] = tb.z; gb[c][3] = tb.w;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) ok &= div_ok(d[c][e]);
+      for (int e = 0; e < 4; ++e) rg.add(d[c][e]);
     }
+    const bool ok = divisor_ok(den) && rg.ok();
     // (a * d) / den: correctly rounded via div_cr unless a value is out of its range
     if (__builtin_expect(__ballot(!ok) == 0ull, 1)) {
       const float y = 1.0f / den;
@@ -507,6 +508,11 @@ hipError_t launch_u8_from_any(const void* src, int elem_bytes, long n, uint8_t* 
 }
 
 __global__ void k_step_inc(int* s) { *s += 1; }
+__global__ void k_nop() {}
+hipError_t launch_nop(hipStream_t st) {   // timing experiments (QTX_ABLATE)
+  k_nop<<<1, 64, 0, st>>>();
+  return hipGetLastError();
+}
 hipError_t launch_step_inc(int* step, hipStream_t st) {
   k_step_inc<<<1, 1, 0, st>>>(step);
   return hipGetLastError();

@@ -71,6 +71,8 @@ def lib(build: bool = True):
     if _lib is not None:
         return _lib
     path = _build.build() if build else _build.LIB
+    if os.environ.get("QTX_LIB_PATH"):        # diagnostic builds (tools/kernel_bench.py)
+        path = os.environ["QTX_LIB_PATH"]
     if not os.path.exists(path):
         raise RuntimeError(f"libqtx.so missing at {path}; run __graft_entry__.build()")
     L = C.CDLL(path)

@@ -64,11 +64,14 @@ def test_greedy_decode_matches_oracle(torch, gpu_model, oracle_model, golden_mod
     np.testing.assert_array_equal(ys, ref)
 
 
-@pytest.mark.parametrize("env", [{"QTX_NO_GRAPH": "1"}, {"QTX_UNFUSED": "1"}])
-def test_greedy_paths_agree(torch, gpu_model, golden_model, monkeypatch, env):
-    """The fused+graph decode step, the fused eager step and the unfused kernels agree."""
+@pytest.mark.parametrize("env", [{"QTX_NO_GRAPH": "1"}, {"QTX_UNFUSED": "1"},
+                                 {"QTX_GRAPH_STEPS": "13"}, {"QTX_DECODE_GROUPS": "3"},
+                                 {"QTX_DECODE_GROUPS": "2", "QTX_NO_GRAPH": "1"}])
+def test_greedy_paths_agree(torch, gpu_model, monkeypatch, env):
+    """The fused+graph decode step, the fused eager step, the unfused kernels, graphs of
+    several steps and sub-batches on several streams agree."""
     from qtx.decode import greedy_decode
-    src, m = golden_model["src"], golden_model["src_mask"]
+    src, m = make_batch(np.random.default_rng(5), 5, 24, lens=[24, 20, 9, 17, 3])
     ref = greedy_decode(gpu_model, src, m, 40, 0)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
