@@ -140,27 +140,30 @@ int32_t qtx_attention_i8(const int8_t* q, const float* sq, const int8_t* k, cons
 
 /* Skinny int8 GEMM for decode (M small): out = epilogue(A . W^T) with the A operand made
  * in the prologue: amode 0 = int8 A [M,K] + sa; 1 = LayerNorm(X [M,512]; ln_a, ln_b) then
- * per-token quant; 2 = fp32 X [M,K] quantized with s = max(rowmax_in, 1e-5)/127
- * (rowmax_in = float bits of the row absmax).  flags: 1 ReLU, 2 residual (res), 4 row
- * absmax of the output into rowmax_out (atomicMax on float bits; zero it first).
- * N % 16 == 0, K in {512, 2048}. */
+ * per-token quant; 2 = fp32 X [M,K] quantized per token with s = max(m, 1e-5)/127 where m =
+ * max over p < pmax_n of pmax_in[p*M + row] (partial row absmaxima, e.g. per head or per
+ * column tile; pmax_n <= 128).  flags: 1 ReLU, 2 residual (res), 4 partial row absmax of
+ * the output per 16-column tile into pmax_out [N/16][M].  N % 16 == 0, K in {512, 2048}
+ * (amode 1: K = 512).  quant_linear.py:111-119, layer_norm.py:12-15. */
 int32_t qtx_skinny_linear(int32_t amode, const int8_t* A, const float* sa, const float* X,
                           int64_t ldx, const float* ln_a, const float* ln_b,
-                          const uint32_t* rowmax_in, const void* W, const float* sw,
+                          const float* pmax_in, int32_t pmax_n, const void* W, const float* sw,
                           const float* bias, int32_t M, int32_t N, int32_t K,
                           int32_t weight_bits, int32_t flags, const float* res, float* out,
-                          uint32_t* rowmax_out, void* stream);
+                          float* pmax_out, void* stream);
 
 /* One-query-per-sentence attention of the decode step (attention.py:23-67).
  * kv_new = 1 (self): y [B, 3*512] holds this step's q|k|v projections; they are quantized
- *   per token, k/v written to the caches at row b*kv_bs + *step_dev, keys 0..*step_dev.
+ *   per token, k/v written to the caches at row b*kv_bs + *step_dev, keys 0..*step_dev
+ *   (kv_bs <= 128).
  * kv_new = 0 (cross): y [B,512] holds q; keys = S cached rows per sentence, mask [B,S].
- * Caches: kc/vc int8 [B][kv_bs][512], skc/svc [B][kv_bs].  Out: quantized context
- * a8 [B,512] + sa [B].  Keys <= 128. */
+ * Caches: kc/vc int8 [B][kv_bs][512], skc/svc [B][kv_bs].  Out: fp32 context ctx [B,512]
+ * and the per-head absmax pmax [8][B] (the next GEMM's per-token quantization, amode 2 of
+ * qtx_skinny_linear with pmax_n = 8).  Keys <= 128. */
 int32_t qtx_decode_attention(int32_t kv_new, const float* y, int64_t ldy, int8_t* kc,
                              int8_t* vc, float* skc, float* svc, int32_t kv_bs,
                              const int32_t* step_dev, int32_t S, const uint8_t* mask,
-                             int32_t B, int8_t* a8, float* sa, void* stream);
+                             int32_t B, float* ctx, float* pmax, void* stream);
 
 #ifdef __cplusplus
 }

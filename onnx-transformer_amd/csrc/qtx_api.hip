@@ -76,9 +76,10 @@ struct DecLayer {
 struct GraphKey {
   int B, S, L, G;
   const void *ws, *ids, *mask;
+  std::string variant;   // the QTX_* experiment switches the captured step depends on
   bool operator<(const GraphKey& o) const {
-    return std::tie(B, S, L, G, ws, ids, mask) <
-           std::tie(o.B, o.S, o.L, o.G, o.ws, o.ids, o.mask);
+    return std::tie(B, S, L, G, ws, ids, mask, variant) <
+           std::tie(o.B, o.S, o.L, o.G, o.ws, o.ids, o.mask, o.variant);
   }
 };
 
@@ -522,7 +523,8 @@ struct GreedyWS {
   float* xo;
   float* logits;
   int* step;          // [0] = decode position, [1] = argmax arrival counter
-  unsigned* rowmax;   // [B] FFN1 row absmax (A_F32Q operand of FFN2)
+  float* pmax_a;      // [8][B]    per-head absmax of the attention context (A_F32Q input)
+  float* pmax_f;      // [F/16][B] per-column-tile absmax of FFN1's output
   // fused-decode sub-batches: step scratch (grp[0] = dec) and step counters, 4 ints each
   std::vector<Scratch> grp;
   int* gsteps;
@@ -562,7 +564,8 @@ GreedyWS carve_greedy(Arena& ar, const qtx_config& c, int B, int S, int max_len)
   g.xo = ar.take<float>((size_t)B * D);
   g.logits = ar.take<float>((size_t)B * c.tgt_vocab);
   g.step = ar.take<int>(4);
-  g.rowmax = ar.take<unsigned>((size_t)B);
+  g.pmax_a = ar.take<float>((size_t)8 * B);
+  g.pmax_f = ar.take<float>((size_t)(c.d_ff / 16) * B);
   const Groups gr = decode_groups(B);
   g.grp.push_back(g.dec);
   for (int i = 1; i < gr.G; ++i) g.grp.push_back(carve_scratch(ar, c, gr.Bg));
@@ -583,7 +586,8 @@ GreedyWS group_view(const GreedyWS& g, const qtx_config& c, int i, int b0, int S
     v.cross.sk[l] += b0 * S; v.cross.sv[l] += b0 * S;
   }
   v.logits += (long)b0 * c.tgt_vocab;
-  v.rowmax += b0;
+  v.pmax_a += (long)8 * b0;               // each sub-batch: its own [P][rows] block
+  v.pmax_f += (long)(c.d_ff / 16) * b0;
   v.step = g.gsteps + 4 * i;
   return v;
 }
@@ -606,8 +610,8 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
                       int64_t* ids, const uint8_t* src_mask, hipStream_t st) {
   const qtx_config& c = m->cfg;
   const int D = c.d_model, F = c.d_ff, wb = c.weight_bits;
-  const bool ffn_rowmax = env_flag("QTX_FFN_ROWMAX");
-  const bool fused_ln = env_flag("QTX_FUSED_LN");
+  const bool ffn_qkernel = env_flag("QTX_FFN_QKERNEL");
+  const bool fused_ln = !env_flag("QTX_SPLIT_LN");
   Scratch& s = g.dec;
   // Timing experiments only (wrong results): QTX_ABLATE=<bitmask> drops kernel classes
   // from the step (replaced by an empty kernel with QTX_ABLATE_NOP=1) to measure what
@@ -624,9 +628,9 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
       HIPCHK(launch);                          \
     }                                          \
   } while (0)
-  // out = epilogue(quant(LN(x)) . W^T): LayerNorm + per-token quant as its own kernel
-  // (one wave per row, 2.7 us) then the int8 GEMM — measured faster than recomputing the
-  // LayerNorm of all rows in every GEMM workgroup (the A_LN prologue, QTX_FUSED_LN=1).
+  // out = epilogue(quant(LN(x)) . W^T): the LayerNorm + per-token quant is recomputed in
+  // the prologue of every GEMM workgroup (4 rows each, A_LN) — cheaper than its own kernel
+  // launch; QTX_SPLIT_LN=1 restores the separate LN kernel (timing experiments).
 #define QTX_RUNRC(bit, expr)                   \
   do {                                         \
     if (abl & (bit)) {                         \
@@ -638,6 +642,7 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
   auto ln_linear = [&](const QLin& W, const float* const* ln, int flags, float* out,
                        long ldo, int bit) -> int {
     SkinnyArgs k = skinny(wb, W, B, fused_ln ? A_LN : A_I8, flags, out, ldo);
+    if (flags & EPI_ROWMAX) k.pmax_out = g.pmax_f;
     if (fused_ln) {
       k.X = s.x; k.ldx = D; k.ln_a = ln[0]; k.ln_b = ln[1];
     } else {
@@ -654,30 +659,27 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
     DecAttnArgs at{};
     at.y = s.y; at.ldy = 3 * D; at.kv_new = 1; at.step = g.step;
     at.kc = g.kc[l]; at.vc = g.vc[l]; at.skc = g.skc[l]; at.svc = g.svc[l]; at.kv_bs = max_len;
-    at.a8 = s.a8; at.sa = s.sa;
+    at.ctx = s.ctx; at.pmax = g.pmax_a; at.B = B;
     QTX_RUN(4, launch_dec_attn(at, B, st));
-    a = skinny(wb, L.o, B, A_I8, EPI_RESIDUAL, s.x, D);
-    a.A = s.a8; a.sa = s.sa; a.res = s.x; a.ldr = D;
+    a = skinny(wb, L.o, B, A_F32Q, EPI_RESIDUAL, s.x, D);   // quantizes ctx per token
+    a.X = s.ctx; a.ldx = D; a.pmax_in = g.pmax_a; a.pmax_n = 8; a.res = s.x; a.ldr = D;
     QTX_RUN(16, launch_skinny(a, wb, st));
     RC(ln_linear(L.cq, L.ln[1], 0, s.y, D, 2));
     at = DecAttnArgs{};
     at.y = s.y; at.ldy = D; at.kv_new = 0; at.S = S; at.mask = src_mask;
     at.kc = g.cross.k8[l]; at.vc = g.cross.v8[l]; at.skc = g.cross.sk[l];
     at.svc = g.cross.sv[l]; at.kv_bs = S;
-    at.a8 = s.a8; at.sa = s.sa;
+    at.ctx = s.ctx; at.pmax = g.pmax_a; at.B = B;
     QTX_RUN(8, launch_dec_attn(at, B, st));
-    a = skinny(wb, L.co, B, A_I8, EPI_RESIDUAL, s.x, D);
-    a.A = s.a8; a.sa = s.sa; a.res = s.x; a.ldr = D;
-    a.zero = g.rowmax; a.zero_n = B;
+    a = skinny(wb, L.co, B, A_F32Q, EPI_RESIDUAL, s.x, D);
+    a.X = s.ctx; a.ldx = D; a.pmax_in = g.pmax_a; a.pmax_n = 8; a.res = s.x; a.ldr = D;
     QTX_RUN(16, launch_skinny(a, wb, st));
-    if (ffn_rowmax) {   // FFN2 quantizes h itself from FFN1's atomic row maxima
-      a = skinny(wb, L.w1, B, A_LN, EPI_RELU | EPI_ROWMAX, s.y, F);
-      a.X = s.x; a.ldx = D; a.ln_a = L.ln[2][0]; a.ln_b = L.ln[2][1]; a.rowmax_out = g.rowmax;
-      QTX_RUN(32, launch_skinny(a, wb, st));
+    if (!ffn_qkernel) {   // FFN2 quantizes h itself from FFN1's per-tile row maxima
+      RC(ln_linear(L.w1, L.ln[2], EPI_RELU | EPI_ROWMAX, s.y, F, 32));
       a = skinny(wb, L.w2, B, A_F32Q, EPI_RESIDUAL, s.x, D);
-      a.X = s.y; a.ldx = F; a.rowmax_in = g.rowmax; a.res = s.x; a.ldr = D;
+      a.X = s.y; a.ldx = F; a.pmax_in = g.pmax_f; a.pmax_n = F / 16; a.res = s.x; a.ldr = D;
       QTX_RUN(128, launch_skinny(a, wb, st));
-    } else {            // one wave per row quantizes h (quant_linear.py:30-43), then FFN2
+    } else {              // one wave per row quantizes h (quant_linear.py:30-43), then FFN2
       RC(ln_linear(L.w1, L.ln[2], EPI_RELU, s.y, F, 32));
       QTX_RUNRC(64, quant(s.y, F, B, F, s.a8, s.sa, st));
       a = skinny(wb, L.w2, B, A_I8, EPI_RESIDUAL, s.x, D);
@@ -895,7 +897,12 @@ int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t*
   if (const char* v = getenv("QTX_GRAPH_STEPS"))
     if (*v && atoi(v) > 0 && (max_len - 1) % atoi(v) == 0) per_graph = atoi(v);
   if (max_len <= 1) return QTX_OK;
-  const GraphKey key{B, S, max_len, gr.G * 1000 + per_graph, ws, ids, src_mask};
+  std::string variant;
+  for (const char* k : {"QTX_SPLIT_LN", "QTX_FFN_QKERNEL", "QTX_ABLATE", "QTX_ABLATE_NOP"}) {
+    const char* v = getenv(k);
+    variant += std::string(k) + "=" + (v ? v : "") + ";";
+  }
+  const GraphKey key{B, S, max_len, gr.G * 1000 + per_graph, ws, ids, src_mask, variant};
   auto it = mm->graphs.find(key);
   if (it == mm->graphs.end()) {
     if (mm->graphs.size() >= 16) mm->clear_graphs();
@@ -1003,21 +1010,23 @@ int32_t qtx_linear_i8(const int8_t* A, const float* sa, const void* W, const flo
 
 int32_t qtx_skinny_linear(int32_t amode, const int8_t* A, const float* sa, const float* X,
                           int64_t ldx, const float* ln_a, const float* ln_b,
-                          const uint32_t* rowmax_in, const void* W, const float* sw,
+                          const float* pmax_in, int32_t pmax_n, const void* W, const float* sw,
                           const float* bias, int32_t M, int32_t N, int32_t K,
                           int32_t weight_bits, int32_t flags, const float* res, float* out,
-                          uint32_t* rowmax_out, void* stream) {
+                          float* pmax_out, void* stream) {
   if (!W || !sw || !bias || !out) return fail(QTX_E_INVALID, "null argument");
   if ((amode == A_I8 && (!A || !sa)) || (amode == A_LN && (!X || !ln_a || !ln_b)) ||
-      (amode == A_F32Q && (!X || !rowmax_in)) || amode < 0 || amode > 2)
+      (amode == A_F32Q && (!X || !pmax_in || pmax_n <= 0 || pmax_n > 128)) || amode < 0 ||
+      amode > 2)
     return fail(QTX_E_INVALID, "operands missing for amode %d", amode);
-  if (((flags & EPI_RESIDUAL) && !res) || ((flags & EPI_ROWMAX) && !rowmax_out))
-    return fail(QTX_E_INVALID, "flags need res / rowmax_out");
+  if (((flags & EPI_RESIDUAL) && !res) || ((flags & EPI_ROWMAX) && !pmax_out))
+    return fail(QTX_E_INVALID, "flags need res / pmax_out");
   SkinnyArgs g{};
   g.amode = amode; g.A = A; g.sa = sa; g.X = X; g.ldx = ldx; g.ln_a = ln_a; g.ln_b = ln_b;
-  g.rowmax_in = rowmax_in; g.W = (const int8_t*)W; g.ldw = weight_bits == 8 ? K : K / 2;
+  g.pmax_in = pmax_in; g.pmax_n = pmax_n;
+  g.W = (const int8_t*)W; g.ldw = weight_bits == 8 ? K : K / 2;
   g.sw = sw; g.bias = bias; g.out = out; g.ldo = N; g.res = res; g.ldr = N;
-  g.rowmax_out = rowmax_out; g.M = M; g.N = N; g.K = K; g.flags = flags;
+  g.pmax_out = pmax_out; g.M = M; g.N = N; g.K = K; g.flags = flags;
   hipError_t e = launch_skinny(g, weight_bits, (hipStream_t)stream);
   if (e == hipErrorInvalidValue)
     return fail(QTX_E_UNSUPPORTED, "skinny: N=%d K=%d amode=%d bits=%d", N, K, amode, weight_bits);
@@ -1028,13 +1037,16 @@ int32_t qtx_skinny_linear(int32_t amode, const int8_t* A, const float* sa, const
 int32_t qtx_decode_attention(int32_t kv_new, const float* y, int64_t ldy, int8_t* kc,
                              int8_t* vc, float* skc, float* svc, int32_t kv_bs,
                              const int32_t* step_dev, int32_t S, const uint8_t* mask,
-                             int32_t B, int8_t* a8, float* sa, void* stream) {
-  if (!y || !kc || !vc || !skc || !svc || !a8 || !sa) return fail(QTX_E_INVALID, "null argument");
-  if (kv_new ? !step_dev : (!mask || S <= 0 || S > 128 || S > kv_bs))
-    return fail(QTX_E_INVALID, "decode attention: bad step/mask/S");
+                             int32_t B, float* ctx, float* pmax, void* stream) {
+  if (!y || !kc || !vc || !skc || !svc || !ctx || !pmax)
+    return fail(QTX_E_INVALID, "null argument");
+  if (kv_new ? (!step_dev || kv_bs <= 0 || kv_bs > 128)
+             : (!mask || S <= 0 || S > 128 || S > kv_bs))
+    return fail(QTX_E_INVALID, "decode attention: bad step/mask/S/kv_bs");
   DecAttnArgs a{};
   a.y = y; a.ldy = ldy; a.kc = kc; a.vc = vc; a.skc = skc; a.svc = svc; a.kv_bs = kv_bs;
-  a.step = step_dev; a.S = S; a.mask = mask; a.a8 = a8; a.sa = sa; a.kv_new = kv_new;
+  a.step = step_dev; a.S = S; a.mask = mask; a.kv_new = kv_new;
+  a.ctx = ctx; a.pmax = pmax; a.B = B;
   HIPCHK(launch_dec_attn(a, B, (hipStream_t)stream));
   return QTX_OK;
 }

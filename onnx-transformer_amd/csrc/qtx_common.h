@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #define QTX_WAVE 64
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -60,6 +62,18 @@ __device__ __forceinline__ float wave_max(float v) {
   v = fmaxf(v, dpp<0x141>(v));
   v = fmaxf(v, dpp<0x140>(v));
   return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
+}
+
+__device__ __forceinline__ int wave_min_i32(int v) {
+  auto d = [](int x, auto ctrl) {
+    return __builtin_amdgcn_update_dpp(0x7fffffff, x, decltype(ctrl)::value, 0xF, 0xF, false);
+  };
+  v = min(v, d(v, std::integral_constant<int, 0xB1>{}));
+  v = min(v, d(v, std::integral_constant<int, 0x4E>{}));
+  v = min(v, d(v, std::integral_constant<int, 0x141>{}));
+  v = min(v, d(v, std::integral_constant<int, 0x140>{}));
+  return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
 
 // ---------------------------------------------------------------- canonical exp

@@ -3,14 +3,17 @@
 //   k_skinny        M<=32-row int8 GEMM, 16 columns per workgroup, K split over 4 waves,
 //                   A operand built in the prologue (int8 | LayerNorm+quant | rowmax-quant)
 //                   quant_linear.py:111-119, layer_norm.py:12-15, position_feed_forward.py:12
-//   k_dec_attn      one query per sentence, 8 heads = 8 waves; quantizes q/k/v per token,
-//                   appends k/v to the cache, attention, quantizes the context row
+//   k_dec_attn      one query per sentence, one wave per (sentence, head); quantizes q/k/v
+//                   per token, appends k/v to the cache, attention; fp32 context + per-head
+//                   absmax for the next GEMM's per-token quantization
 //                   attention.py:23-67, get_quantized_model.py:160-168
 //   k_generator_ln  final LayerNorm fused into the fp32 generator projection  generator.py:14-15
 //   k_argmax_embed  log_softmax + first argmax + next-token embedding + step advance
 //                   onnx_reference_inference.py:632,640-643
 //
 // All float steps follow the canonical order shared with oracle/qtx_oracle.py.
+#include <cstdlib>
+
 #include "qtx_common.h"
 #include "qtx_kernels.h"
 
@@ -135,9 +138,10 @@ __device__ __forceinline__ void quant_rows512(const float (&v)[R][2][4], uint32_
 // =====================================================================================
 // k_skinny
 // =====================================================================================
-template <int MF, int K, int WBITS, int AMODE, int FLAGS>
+template <int MF, int RB, int K, int WBITS, int AMODE, int FLAGS>
 __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
-  constexpr int BM = 16 * MF;
+  constexpr int BM = 16 * MF;     // MFMA rows (rows >= RB of the A panel are don't-care)
+  static_assert(RB % 4 == 0 && RB <= BM, "rows per block");
   constexpr int KW = K / 4;       // K range of one wave
   constexpr int NS = KW / 64;     // MFMA k-steps per wave
   constexpr int LDA = K + 16;     // padded LDS row (bytes)
@@ -147,11 +151,9 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
-  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * BM;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * RB;
 
   QTX_STAMP(0);
-  if (g.zero && blockIdx.x == 0 && blockIdx.y == 0)
-    for (int i = tid; i < g.zero_n; i += 256) g.zero[i] = 0u;
 
   // 1. this lane's W fragments for its wave's K range, issued first
   const int n = min(n0 + fr, g.N - 1);
@@ -178,28 +180,31 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
     for (int i = 0; i < MF; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int row = m0 + 16 * i + 4 * fg + e;
-        rv[i][e] = (resid && cok && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
+        const int r = 16 * i + 4 * fg + e, row = m0 + r;
+        rv[i][e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
       }
   }
 
   // 2. A panel (int8) and per-row scales into LDS.  Every branch issues all of its
   //    global loads before consuming any (one memory latency, not one per row).
-  constexpr int RPW = BM / 4;  // rows per wave: r = wave + 4*j
+  constexpr int RPW = RB / 4;  // rows per wave: r = wave + 4*j
   if constexpr (AMODE == A_I8) {
-    constexpr int CPR = K / 16, NLD = BM * CPR / 256;
+    // the panel is RB*K/16 uint4; the index is clamped (a duplicate load, no divergent
+    // branch around the load) and only in-range indices are stored
+    constexpr int CPR = K / 16, TOT = RB * CPR, NLD = (TOT + 255) / 256;
     uint4 v[NLD];
 #pragma unroll
     for (int j = 0; j < NLD; ++j) {
-      const int idx = tid + 256 * j, m = min(m0 + idx / CPR, g.M - 1);
+      const int idx = min(tid + 256 * j, TOT - 1), m = min(m0 + idx / CPR, g.M - 1);
       v[j] = *reinterpret_cast<const uint4*>(g.A + (long)m * K + 16 * (idx % CPR));
     }
-    if (tid < BM) sas[tid] = (m0 + tid < g.M) ? g.sa[m0 + tid] : 0.0f;
+    if (tid < BM) sas[tid] = (tid < RB && m0 + tid < g.M) ? g.sa[m0 + tid] : 0.0f;
 #pragma unroll
     for (int j = 0; j < NLD; ++j) {
       const int idx = tid + 256 * j, r = idx / CPR;
-      *reinterpret_cast<uint4*>(As + r * LDA + 16 * (idx % CPR)) =
-          (m0 + r < g.M) ? v[j] : make_uint4(0, 0, 0, 0);
+      if (TOT % 256 == 0 || idx < TOT)
+        *reinterpret_cast<uint4*>(As + r * LDA + 16 * (idx % CPR)) =
+            (m0 + r < g.M) ? v[j] : make_uint4(0, 0, 0, 0);
     }
   } else if constexpr (AMODE == A_LN) {
     float v[RPW][2][4];
@@ -225,24 +230,27 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
       dst[lane + 64] = ok ? q[j][1] : 0u;
       if (lane == 0) sas[r] = ok ? sc[j] : 0.0f;
     }
-  } else {  // A_F32Q: rows in batches of 4 (32 float4 in flight per lane at K = 2048)
-    constexpr int NC = K / 256, RB = RPW < 4 ? RPW : 4;
+  } else {  // A_F32Q: each wave's rows (<= 4 at a time) with their partial maxima
+    constexpr int NC = K / 256, RBT = RPW < 4 ? RPW : 4;
 #pragma unroll
-    for (int j0 = 0; j0 < RPW; j0 += RB) {
-      float4 t[RB][NC];
-      float sc[RB];
+    for (int j0 = 0; j0 < RPW; j0 += RBT) {
+      float4 t[RBT][NC];
+      float pm[RBT][2];
 #pragma unroll
-      for (int jb = 0; jb < RB; ++jb) {
+      for (int jb = 0; jb < RBT; ++jb) {
         const int m = min(m0 + wave + 4 * (j0 + jb), g.M - 1);
-        sc[jb] = quant_scale(__uint_as_float(g.rowmax_in[m]), 127.0f);
 #pragma unroll
         for (int c = 0; c < NC; ++c)
           t[jb][c] = *reinterpret_cast<const float4*>(g.X + (long)m * g.ldx + 4 * (lane + 64 * c));
+#pragma unroll
+        for (int u = 0; u < 2; ++u)   // lane takes partials lane, lane+64 (clamped: max-safe)
+          pm[jb][u] = g.pmax_in[(long)min(lane + 64 * u, g.pmax_n - 1) * g.M + m];
       }
 #pragma unroll
-      for (int jb = 0; jb < RB; ++jb) {
+      for (int jb = 0; jb < RBT; ++jb) {
         const int r = wave + 4 * (j0 + jb);
         const bool ok = m0 + r < g.M;
+        const float sc = quant_scale(wave_max(fmaxf(pm[jb][0], pm[jb][1])), 127.0f);
         uint32_t* dst = reinterpret_cast<uint32_t*>(As + r * LDA);
         float tf[4 * NC];
 #pragma unroll
@@ -251,10 +259,10 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
           tf[4 * c + 2] = t[jb][c].z; tf[4 * c + 3] = t[jb][c].w;
         }
         uint32_t qd[NC];
-        quant_pack<4 * NC>(tf, sc[jb], qd);
+        quant_pack<4 * NC>(tf, sc, qd);
 #pragma unroll
         for (int c = 0; c < NC; ++c) dst[lane + 64 * c] = ok ? qd[c] : 0u;
-        if (lane == 0) sas[r] = ok ? sc[jb] : 0.0f;
+        if (lane == 0) sas[r] = ok ? sc : 0.0f;
       }
     }
   }
@@ -300,18 +308,18 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int r = 16 * i + 4 * fg + e, row = m0 + r;
-      const bool ok = cok && row < g.M;
+      const bool ok = cok && r < RB && row < g.M;
       float y = ((float)acc[i][e] * sas[r]) * swc + bc;
       if constexpr (relu) y = y > 0.0f ? y : 0.0f;
       if constexpr (resid) y = rv[i][e] + y;
       if (ok) g.out[(long)row * g.ldo + col] = y;
       if constexpr (rmax) {
-        float am = ok ? fabsf(y) : 0.0f;
-        am = fmaxf(am, __shfl_xor(am, 8, 64));
-        am = fmaxf(am, __shfl_xor(am, 4, 64));
-        am = fmaxf(am, __shfl_xor(am, 2, 64));
-        am = fmaxf(am, __shfl_xor(am, 1, 64));
-        if (fr == 0 && row < g.M) atomicMax(g.rowmax_out + row, __float_as_uint(am));
+        float am = ok ? fabsf(y) : 0.0f;   // max over the 16 lanes (columns) of this row
+        am = fmaxf(am, dpp<0xB1>(am));
+        am = fmaxf(am, dpp<0x4E>(am));
+        am = fmaxf(am, dpp<0x141>(am));
+        am = fmaxf(am, dpp<0x140>(am));
+        if (fr == 0 && r < RB && row < g.M) g.pmax_out[(long)blockIdx.x * g.M + row] = am;
       }
     }
   }
@@ -320,28 +328,53 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
 
 // dispatch: the prologue mode and epilogue flags are template parameters (no runtime
 // branches per output element).  Supported: K 512 with A_I8 / A_LN, K 2048 with A_I8 /
-// A_F32Q; flags 0, RELU, RESIDUAL, RELU|ROWMAX.
-template <int MF, int K, int WB, int AM>
-hipError_t skinny_flags(const SkinnyArgs& g, dim3 grid, hipStream_t st) {
+// A_F32Q; flags 0, RELU, RESIDUAL, RELU|ROWMAX.  Rows per workgroup RB: 16*MF for an int8
+// A panel; 4 (one row per wave) for the LayerNorm prologue, which re-normalizes its rows
+// in every column workgroup — few rows per workgroup keeps that short and spreads the
+// fp32 row reads over many CUs (measured: RB 32 -> 8 -> 4 = 11.0 -> 5.1 -> 4.6 us for
+// N=1536, M=32; in the decode step the fused form beats LN kernel + GEMM).
+template <int MF, int RB, int K, int WB, int AM>
+hipError_t skinny_flags(const SkinnyArgs& g, hipStream_t st) {
+  const dim3 grid(g.N / 16, (g.M + RB - 1) / RB);
   switch (g.flags) {
-    case 0: k_skinny<MF, K, WB, AM, 0><<<grid, 256, 0, st>>>(g); break;
-    case EPI_RELU: k_skinny<MF, K, WB, AM, EPI_RELU><<<grid, 256, 0, st>>>(g); break;
-    case EPI_RESIDUAL: k_skinny<MF, K, WB, AM, EPI_RESIDUAL><<<grid, 256, 0, st>>>(g); break;
+    case 0: k_skinny<MF, RB, K, WB, AM, 0><<<grid, 256, 0, st>>>(g); break;
+    case EPI_RELU: k_skinny<MF, RB, K, WB, AM, EPI_RELU><<<grid, 256, 0, st>>>(g); break;
+    case EPI_RESIDUAL: k_skinny<MF, RB, K, WB, AM, EPI_RESIDUAL><<<grid, 256, 0, st>>>(g); break;
     case EPI_RELU | EPI_ROWMAX:
-      k_skinny<MF, K, WB, AM, EPI_RELU | EPI_ROWMAX><<<grid, 256, 0, st>>>(g);
+      k_skinny<MF, RB, K, WB, AM, EPI_RELU | EPI_ROWMAX><<<grid, 256, 0, st>>>(g);
       break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
-template <int MF, int WB>
-hipError_t skinny_mode(const SkinnyArgs& g, dim3 grid, hipStream_t st) {
+template <int K, int WB, int AM>
+hipError_t skinny_rb(const SkinnyArgs& g, int rb, hipStream_t st) {
+  switch (rb) {
+    case 4: return skinny_flags<1, 4, K, WB, AM>(g, st);
+    case 8: return skinny_flags<1, 8, K, WB, AM>(g, st);
+    case 16: return skinny_flags<1, 16, K, WB, AM>(g, st);
+    case 32: return skinny_flags<2, 32, K, WB, AM>(g, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+int env_rb(const char* name, int def) {   // experiment overrides (QTX_RB_*)
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : def;
+}
+// Rows per workgroup (decode step, M = 32, measured in bench.py): small row blocks spread
+// the A-panel and weight reads over more CUs — each CU sustains only a few KB in flight,
+// so a latency-bound kernel is fastest when every workgroup touches ~10-40 KB.
+template <int WB>
+hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
   if (g.K == 512) {
-    if (g.amode == A_I8) return skinny_flags<MF, 512, WB, A_I8>(g, grid, st);
-    if (g.amode == A_LN) return skinny_flags<MF, 512, WB, A_LN>(g, grid, st);
+    static const int rb_i8 = env_rb("QTX_RB_I8_512", 8), rb_ln = env_rb("QTX_RB_LN", 4);
+    if (g.amode == A_I8) return skinny_rb<512, WB, A_I8>(g, g.M <= 4 ? 4 : rb_i8, st);
+    if (g.amode == A_LN) return skinny_rb<512, WB, A_LN>(g, rb_ln, st);
+    if (g.amode == A_F32Q) return skinny_rb<512, WB, A_F32Q>(g, g.M <= 4 ? 4 : rb_i8, st);
   } else if (g.K == 2048) {
-    if (g.amode == A_I8) return skinny_flags<MF, 2048, WB, A_I8>(g, grid, st);
-    if (g.amode == A_F32Q) return skinny_flags<MF, 2048, WB, A_F32Q>(g, grid, st);
+    static const int rb_i8 = env_rb("QTX_RB_I8_2048", 4), rb_f = env_rb("QTX_RB_F32Q", 4);
+    if (g.amode == A_I8) return skinny_rb<2048, WB, A_I8>(g, rb_i8, st);
+    if (g.amode == A_F32Q) return skinny_rb<2048, WB, A_F32Q>(g, rb_f, st);
   }
   return hipErrorInvalidValue;
 }
@@ -349,159 +382,189 @@ hipError_t skinny_mode(const SkinnyArgs& g, dim3 grid, hipStream_t st) {
 hipError_t launch_skinny(const SkinnyArgs& g, int wbits, hipStream_t st) {
   if (g.M <= 0) return hipSuccess;
   if (g.N % 16) return hipErrorInvalidValue;
-  const int MF = g.M <= 16 ? 1 : 2;
-  const dim3 grid(g.N / 16, (g.M + 16 * MF - 1) / (16 * MF));
-  if (wbits == 8) return MF == 1 ? skinny_mode<1, 8>(g, grid, st) : skinny_mode<2, 8>(g, grid, st);
-  if (wbits == 4) return MF == 1 ? skinny_mode<1, 4>(g, grid, st) : skinny_mode<2, 4>(g, grid, st);
+  if (wbits == 8) return skinny_mode<8>(g, st);
+  if (wbits == 4) return skinny_mode<4>(g, st);
   return hipErrorInvalidValue;
 }
 
 // =====================================================================================
-// k_dec_attn: 512 threads = 8 waves; wave h = head h.  Keys staged in LDS (<= 128).
+// k_dec_attn: one wave per (sentence, head) — 8*B workgroups, so the cached keys/values
+// (the bulk of the bytes) are spread over many CUs instead of one CU per sentence.  Each
+// wave quantizes the q (and new k/v) row itself (full-row maxima recomputed per head:
+// 2-6 KB of reads), attends over its head and writes its 64 fp32 context values plus
+// their absmax; the per-token quantization of the context row happens in the prologue of
+// the output-projection GEMM (A_F32Q), so no cross-workgroup step is needed here.
+// Keys staged in LDS (<= 128).  Grid (B, 8): the 8 heads of sentence b share blockIdx.x,
+// so with B % 8 == 0 they land on one XCD (workgroups go round-robin over the 8 XCDs).
 // =====================================================================================
 constexpr int DEC_MAXK = 128;
 
-// block-wide max of one value per thread (512 threads), result broadcast
-__device__ __forceinline__ float block_max512(float v, float* scratch) {
-  v = wave_max(v);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  __syncthreads();
-  if (l == 0) scratch[w] = v;
-  __syncthreads();
-  float m = scratch[0];
-#pragma unroll
-  for (int i = 1; i < 8; ++i) m = fmaxf(m, scratch[i]);
-  return m;
-}
-
-template <bool KV_NEW>
-__global__ __launch_bounds__(512) void k_dec_attn(DecAttnArgs a) {
-  __shared__ uint32_t Ks[8][DEC_MAXK * 17];     // per head: key rows of 64 int8 (+4 B pad)
-  __shared__ __attribute__((aligned(16))) uint8_t Vs[DEC_MAXK * 512];
-  __shared__ float sks[DEC_MAXK], svs[DEC_MAXK];
-  __shared__ float Pb[8][DEC_MAXK];
-  __shared__ float red[3][8];
-  __shared__ __attribute__((aligned(16))) int8_t qrow[512];   // read back as dwords
-  const int b = blockIdx.x, t = threadIdx.x, h = t >> 6, lane = t & 63;
+template <bool KV_NEW, int NIT>
+__global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
+  __shared__ uint32_t Ks[DEC_MAXK * 17];   // key rows of this head: 16 dwords (+1 pad)
+  __shared__ __attribute__((aligned(16))) uint8_t Vs[DEC_MAXK * 64];
+  __shared__ float sks[DEC_MAXK], svs[DEC_MAXK], P[DEC_MAXK];
+  __shared__ __attribute__((aligned(16))) int8_t qs[64];
+  const int b = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
   QTX_STAMP(0);
   const float* yr = a.y + (long)b * a.ldy;
+  const int nrows = KV_NEW ? (int)a.kv_bs : a.S;   // rows staged (self: all allocated rows)
+  const long kvb = (long)b * a.kv_bs;
+
+  // phase 0: every global load first (one memory latency).  Key/value row r of this head
+  // = 4 uint4; lane takes row 16*i + lane/4, chunk lane%4 (clamped: no divergent loads).
+  const int rsub = lane >> 2, ch = lane & 3;
+  uint4 kr[NIT], vr[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int r = min(16 * i + rsub, nrows - 1);
+    const long off = (kvb + r) * 512 + h * 64 + 16 * ch;
+    kr[i] = *reinterpret_cast<const uint4*>(a.kc + off);
+    vr[i] = *reinterpret_cast<const uint4*>(a.vc + off);
+  }
+  const int j0 = min(lane, nrows - 1), j1 = min(lane + 64, nrows - 1);
+  const float sk0 = a.skc[kvb + j0], sk1 = a.skc[kvb + j1];
+  const float sv0 = a.svc[kvb + j0], sv1 = a.svc[kvb + j1];
+  bool keep0 = true, keep1 = true;
+  if constexpr (!KV_NEW) {
+    keep0 = a.mask[(long)b * a.S + j0] != 0;
+    keep1 = a.mask[(long)b * a.S + j1] != 0;
+  }
+  float4 yq[2], yk[2], yv[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    yq[c] = *reinterpret_cast<const float4*>(yr + 4 * (lane + 64 * c));
+    if constexpr (KV_NEW) {
+      yk[c] = *reinterpret_cast<const float4*>(yr + 512 + 4 * (lane + 64 * c));
+      yv[c] = *reinterpret_cast<const float4*>(yr + 1024 + 4 * (lane + 64 * c));
+    }
+  }
+  const float q_own = yr[h * 64 + lane];
+  const float k_own = KV_NEW ? yr[512 + h * 64 + lane] : 0.0f;
+  const float v_own = KV_NEW ? yr[1024 + h * 64 + lane] : 0.0f;
   const int step = KV_NEW ? *a.step : 0;
   const int Sk = KV_NEW ? step + 1 : a.S;
 
-  // phase 0: issue the loads of the cached keys/values first (one memory latency):
-  // row j = 32 uint4 of K and of V; thread t takes uint4 index t + 512*i
-  const int nk = KV_NEW ? step : a.S;
-  const uint4* kb4 = reinterpret_cast<const uint4*>(a.kc + (long)b * a.kv_bs * 512);
-  const uint4* vb4 = reinterpret_cast<const uint4*>(a.vc + (long)b * a.kv_bs * 512);
-  constexpr int NLD = DEC_MAXK * 32 / 512;
-  // Loads sit behind a wave-uniform bound on the iteration and read a clamped index (row
-  // 0 always exists): a load under a divergent branch makes the compiler wait for it
-  // before the join, serializing them; unconditional clamped loads waste L1 bandwidth.
-  const int lastk = nk * 32 > 0 ? nk * 32 - 1 : 0;
-  const int nit = (nk * 32 + 511) >> 9;
-  uint4 kr[NLD], vr[NLD];
+  // phase 1: per-token scales of q (and k, v) over the full 512-wide rows
+  auto amax8 = [](const float4 (&v)[2]) {
+    float m = 0.0f;
 #pragma unroll
-  for (int i = 0; i < NLD; ++i) {
-    if (i < nit) {
-      const int idx = min(t + 512 * i, lastk);
-      kr[i] = kb4[idx];
-      vr[i] = vb4[idx];
-    }
-  }
-  const int tj = min(t, nk > 0 ? nk - 1 : 0);
-  const float skj = a.skc[(long)b * a.kv_bs + tj];
-  const float svj = a.svc[(long)b * a.kv_bs + tj];
-
-  // phase 1: per-token quantization of the new q (and k, v) rows: one block reduction
-  // for the three row maxima
-  const float vq = yr[t];
-  const float vk = KV_NEW ? yr[512 + t] : 0.0f, vv = KV_NEW ? yr[1024 + t] : 0.0f;
-  {
-    const float wq = wave_max(fabsf(vq)), wk = wave_max(fabsf(vk)), wv = wave_max(fabsf(vv));
-    if (lane == 0) { red[0][h] = wq; red[1][h] = wk; red[2][h] = wv; }
-  }
-  __syncthreads();
-  float amq = red[0][0], amk = red[1][0], amv = red[2][0];
-#pragma unroll
-  for (int i = 1; i < 8; ++i) {
-    amq = fmaxf(amq, red[0][i]); amk = fmaxf(amk, red[1][i]); amv = fmaxf(amv, red[2][i]);
-  }
-  const float sq = quant_scale(amq, 127.0f);
-  qrow[t] = (int8_t)quant_one(vq, sq);
+    for (int c = 0; c < 2; ++c)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[c].x), fabsf(v[c].y)), fmaxf(fabsf(v[c].z), fabsf(v[c].w))));
+    return wave_max(m);
+  };
+  const float sq = quant_scale(amax8(yq), 127.0f);
+  qs[lane] = (int8_t)quant_one(q_own, sq);
+  int8_t kq = 0, vq = 0;
+  float sk = 0.0f, sv = 0.0f;
   if constexpr (KV_NEW) {
-    const float sk = quant_scale(amk, 127.0f), sv = quant_scale(amv, 127.0f);
-    const int8_t qk = (int8_t)quant_one(vk, sk), qv = (int8_t)quant_one(vv, sv);
-    const long row = (long)b * a.kv_bs + step;
-    a.kc[row * 512 + t] = qk;
-    a.vc[row * 512 + t] = qv;
-    reinterpret_cast<int8_t*>(Ks[h])[step * 68 + lane] = qk;
-    Vs[step * 512 + t] = (uint8_t)qv;
-    if (t == 0) {
-      a.skc[row] = sk; a.svc[row] = sv;
-      sks[step] = sk; svs[step] = sv;
-    }
+    sk = quant_scale(amax8(yk), 127.0f);
+    sv = quant_scale(amax8(yv), 127.0f);
+    kq = (int8_t)quant_one(k_own, sk);
+    vq = (int8_t)quant_one(v_own, sv);
+    const long row = kvb + step;
+    a.kc[row * 512 + h * 64 + lane] = kq;     // cache append (attention.py: k/v of this step)
+    a.vc[row * 512 + h * 64 + lane] = vq;
+    if (h == 0 && lane == 0) { a.skc[row] = sk; a.svc[row] = sv; }
   }
-  // phase 2: cached keys 0 .. nk-1 from registers into LDS
+
+  // phase 2: staged rows into LDS, then (self) the new row over the stale one
 #pragma unroll
-  for (int i = 0; i < NLD; ++i) {
-    const int idx = t + 512 * i;
-    if (idx < nk * 32) {
-      const int j = idx >> 5, q = idx & 31;      // q-th uint4 of row j = dwords 4q..4q+3
-      uint32_t* kd = &Ks[q >> 2][j * 17 + 4 * (q & 3)];
-      kd[0] = kr[i].x; kd[1] = kr[i].y; kd[2] = kr[i].z; kd[3] = kr[i].w;
-      reinterpret_cast<uint4*>(Vs + j * 512)[q] = vr[i];
-    }
+  for (int i = 0; i < NIT; ++i) {
+    const int r = min(16 * i + rsub, nrows - 1);
+    uint32_t* kd = &Ks[r * 17 + 4 * ch];
+    kd[0] = kr[i].x; kd[1] = kr[i].y; kd[2] = kr[i].z; kd[3] = kr[i].w;
+    *reinterpret_cast<uint4*>(Vs + r * 64 + 16 * ch) = vr[i];
   }
-  if (t < nk) { sks[t] = skj; svs[t] = svj; }
+  sks[j0] = sk0; sks[j1] = sk1; svs[j0] = sv0; svs[j1] = sv1;
   __syncthreads();
+  if constexpr (KV_NEW) {
+    reinterpret_cast<int8_t*>(&Ks[step * 17])[lane] = kq;
+    Vs[step * 64 + lane] = (uint8_t)vq;
+    if (lane == 0) { sks[step] = sk; svs[step] = sv; }
+    __syncthreads();
+  }
   QTX_STAMP(1);
 
-  // phase 3: head h
+  // phase 3: scores (lane owns keys lane, lane+64), softmax, P quantization
   uint32_t qd[16];
 #pragma unroll
-  for (int w = 0; w < 16; ++w) qd[w] = reinterpret_cast<const uint32_t*>(qrow + h * 64)[w];
-  float* P = Pb[h];
-  const uint8_t* mk = KV_NEW ? nullptr : a.mask + (long)b * a.S;
+  for (int w = 0; w < 16; ++w) qd[w] = reinterpret_cast<const uint32_t*>(qs)[w];
   float lmax = -3.0e38f;
-  for (int j = lane; j < Sk; j += 64) {
-    int acc = 0;
 #pragma unroll
-    for (int w = 0; w < 16; ++w) acc = __builtin_amdgcn_sdot4(qd[w], Ks[h][j * 17 + w], acc, false);
-    float s = (((float)acc * sq) * sks[j]) * 0.125f;
-    if (mk && mk[j] == 0) s = -1.0e9f;
-    P[j] = s;
-    lmax = fmaxf(lmax, s);
+  for (int u = 0; u < 2; ++u) {
+    const int j = lane + 64 * u;
+    if (j < Sk) {
+      int acc = 0;
+#pragma unroll
+      for (int w = 0; w < 16; ++w) acc = __builtin_amdgcn_sdot4(qd[w], Ks[j * 17 + w], acc, false);
+      float s = (((float)acc * sq) * sks[j]) * 0.125f;
+      if (!(u ? keep1 : keep0)) s = -1.0e9f;
+      P[j] = s;
+      lmax = fmaxf(lmax, s);
+    }
   }
   const float m = wave_max(lmax);
   float lsum = 0.0f;
-  for (int j = lane; j < Sk; j += 64) {
-    const float e = qexp(P[j] - m);
-    P[j] = e;
-    lsum = lsum + e;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = lane + 64 * u;
+    if (j < Sk) {
+      const float e = qexp(P[j] - m);
+      P[j] = e;
+      lsum = lsum + e;
+    }
   }
   const float den = wave_sum(lsum);
-  for (int j = lane; j < Sk; j += 64) P[j] = rintf((P[j] / den) * 127.0f) / 127.0f;
-  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = lane + 64 * u;
+    if (j < Sk) P[j] = rintf((P[j] / den) * 127.0f) / 127.0f;
+  }
+  __syncthreads();
   QTX_STAMP(2);
+
+  // phase 4: context dim h*64 + lane = sequential fma chain over the keys
   float acc = 0.0f;
 #pragma unroll 8
   for (int j = 0; j < Sk; ++j)
-    acc = fmaf(P[j], (float)(int8_t)Vs[j * 512 + t] * svs[j], acc);
+    acc = fmaf(P[j], (float)(int8_t)Vs[j * 64 + lane] * svs[j], acc);
   QTX_STAMP(3);
 
-  // phase 4: quantize the context row (all heads) per token -> next GEMM's A operand
-  const float sc = quant_scale(block_max512(fabsf(acc), red[0]), 127.0f);
-  a.a8[(long)b * 512 + t] = (int8_t)quant_one(acc, sc);
-  if (t == 0) a.sa[b] = sc;
+  // phase 5: this head's 64 context values and their absmax; the consumer GEMM takes the
+  // row maximum over the 8 heads and quantizes the row per token (A_F32Q prologue)
+  a.ctx[(long)b * 512 + h * 64 + lane] = acc;
+  const float am = wave_max(fabsf(acc));
+  if (lane == 0) a.pmax[(long)h * a.B + b] = am;
   QTX_STAMP(4);
+}
+
+template <bool KV_NEW>
+hipError_t dec_attn_nit(const DecAttnArgs& a, int B, int nrows, hipStream_t st) {
+  const dim3 grid(B, 8), block(64);
+  switch ((nrows + 15) / 16) {
+    case 1: k_dec_attn<KV_NEW, 1><<<grid, block, 0, st>>>(a); break;
+    case 2: k_dec_attn<KV_NEW, 2><<<grid, block, 0, st>>>(a); break;
+    case 3: k_dec_attn<KV_NEW, 3><<<grid, block, 0, st>>>(a); break;
+    case 4: k_dec_attn<KV_NEW, 4><<<grid, block, 0, st>>>(a); break;
+    case 5: k_dec_attn<KV_NEW, 5><<<grid, block, 0, st>>>(a); break;
+    case 6: k_dec_attn<KV_NEW, 6><<<grid, block, 0, st>>>(a); break;
+    case 7: k_dec_attn<KV_NEW, 7><<<grid, block, 0, st>>>(a); break;
+    case 8: k_dec_attn<KV_NEW, 8><<<grid, block, 0, st>>>(a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st) {
   if (B <= 0) return hipSuccess;
-  if (!a.kv_new && (a.S <= 0 || a.S > DEC_MAXK)) return hipErrorInvalidValue;
-  if (a.kv_new) k_dec_attn<true><<<dim3(B), dim3(512), 0, st>>>(a);
-  else k_dec_attn<false><<<dim3(B), dim3(512), 0, st>>>(a);
-  return hipGetLastError();
+  if (!a.ctx || !a.pmax || a.B != B) return hipErrorInvalidValue;
+  if (a.kv_new) {
+    if (a.kv_bs <= 0 || a.kv_bs > DEC_MAXK) return hipErrorInvalidValue;
+    return dec_attn_nit<true>(a, B, (int)a.kv_bs, st);
+  }
+  if (a.S <= 0 || a.S > DEC_MAXK) return hipErrorInvalidValue;
+  return dec_attn_nit<false>(a, B, a.S, st);
 }
 
 // =====================================================================================
@@ -662,93 +725,96 @@ hipError_t launch_transpose(const float* in, int R, int Cc, float* out, hipStrea
 }
 
 // =====================================================================================
-// k_argmax_embed: one workgroup per row.  The row of logits is staged in LDS (all loads
-// in flight), wave 0 runs the canonical reductions, then the block writes the next
-// decoder input.
+// k_argmax_embed: one 1024-thread workgroup per row.  The row of logits stays in
+// registers (8 per thread, all loads in flight at once); only the exponentials go through
+// LDS, for the canonical lane-split denominator (wave 0).  Then the first argmax of logp,
+// and the block writes the next decoder input.
 // =====================================================================================
-constexpr int ARG_MAXV = 8192;
+constexpr int ARG_T = 1024, ARG_NV = 8, ARG_MAXV = ARG_T * ARG_NV;
 
-__global__ __launch_bounds__(256) void k_argmax_embed(const float* logits, int V, int64_t* ids,
-                                                      long ids_bs, int* step, unsigned* arrive,
-                                                      const float* lut, const float* pe,
-                                                      int max_pos, float* xnext) {
-  __shared__ float Lg[ARG_MAXV];
+__global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int V, int64_t* ids,
+                                                       long ids_bs, int* step, unsigned* arrive,
+                                                       const float* lut, const float* pe,
+                                                       int max_pos, float* xnext) {
   __shared__ float Ev[ARG_MAXV];
-  __shared__ float red[5], redv[4];
-  __shared__ int redi[4], bsh;
-  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  __shared__ float red[16], redv[16], lse_s;
+  __shared__ int redi[16], bsh;
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  QTX_STAMP(0);
   const int s = *step;
   const float* x = logits + (long)m * V;
+  float4 pe_row = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // position s+1 is known up front
+  if (tid < 128) pe_row = *reinterpret_cast<const float4*>(pe + (long)min(s + 1, max_pos - 1) * 512 + 4 * tid);
+  float t[ARG_NV];
 #pragma unroll
-  for (int i = 0; i < ARG_MAXV / 256; ++i) {
-    const int v = tid + 256 * i;
-    if (v < V) Lg[v] = x[v];
-  }
-  // max: order-free, whole block
+  for (int i = 0; i < ARG_NV; ++i) t[i] = x[min(tid + ARG_T * i, V - 1)];   // clamped
+  QTX_STAMP(1);
+  // max: order-free
   float lm = -3.0e38f;
 #pragma unroll
-  for (int i = 0; i < ARG_MAXV / 256; ++i) {
-    const int v = tid + 256 * i;
-    if (v < V) lm = fmaxf(lm, Lg[v]);
-  }
+  for (int i = 0; i < ARG_NV; ++i)
+    if (tid + ARG_T * i < V) lm = fmaxf(lm, t[i]);
   lm = wave_max(lm);
-  if (lane == 0) red[tid >> 6] = lm;
+  if (lane == 0) red[w] = lm;
   __syncthreads();
-  const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  // e_v = qexp(x_v - max) by the whole block, in place
+  float mx = red[0];
 #pragma unroll
-  for (int i = 0; i < ARG_MAXV / 256; ++i) {
-    const int v = tid + 256 * i;
-    if (v < V) Ev[v] = qexp(Lg[v] - mx);
+  for (int i = 1; i < 16; ++i) mx = fmaxf(mx, red[i]);
+  // e_v = qexp(x_v - max) into LDS for the ordered sum
+#pragma unroll
+  for (int i = 0; i < ARG_NV; ++i) {
+    const int v = tid + ARG_T * i;
+    if (v < V) Ev[v] = qexp(t[i] - mx);
   }
   __syncthreads();
+  QTX_STAMP(2);
   // canonical denominator: lane l sums e[l], e[l+64], ... in order (one wave), then tree
-  if (tid < 64) {
+  if (w == 0) {
     float ls = 0.0f;
 #pragma unroll 8
     for (int v = lane; v < V; v += 64) ls = ls + Ev[v];
     ls = wave_sum(ls);
-    if (lane == 0) red[4] = logf(ls);
+    if (lane == 0) lse_s = logf(ls);
   }
   __syncthreads();
-  const float lse = red[4];
-  // first argmax of logp = (x - max) - lse (torch.max tie rule), block-wide
+  const float lse = lse_s;
+  QTX_STAMP(3);
+  // first argmax of logp = (x - max) - lse (torch.max tie rule)
   float best = -3.0e38f;
   int bi = 0x7fffffff;
 #pragma unroll
-  for (int i = 0; i < ARG_MAXV / 256; ++i) {
-    const int v = tid + 256 * i;
+  for (int i = 0; i < ARG_NV; ++i) {
+    const int v = tid + ARG_T * i;
     if (v < V) {
-      const float lp = (Lg[v] - mx) - lse;
+      const float lp = (t[i] - mx) - lse;
       if (lp > best) { best = lp; bi = v; }
     }
   }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const float ob = __shfl_xor(best, off, 64);
-    const int oi = __shfl_xor(bi, off, 64);
-    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-  }
-  if (lane == 0) { redv[tid >> 6] = best; redi[tid >> 6] = bi; }
+  // wave: the maximum, then the smallest index holding it (DPP trees, no LDS round trips)
+  const float wb = wave_max(best);
+  const int wi = wave_min_i32(best == wb ? bi : 0x7fffffff);
+  if (lane == 0) { redv[w] = wb; redi[w] = wi; }
   __syncthreads();
   if (tid == 0) {
     best = redv[0]; bi = redi[0];
-    for (int w = 1; w < 4; ++w)
-      if (redv[w] > best || (redv[w] == best && redi[w] < bi)) { best = redv[w]; bi = redi[w]; }
+    for (int k = 1; k < 16; ++k)
+      if (redv[k] > best || (redv[k] == best && redi[k] < bi)) { best = redv[k]; bi = redi[k]; }
     bi = min(bi, V - 1);   // all-NaN row guard: keep the embedding gather in bounds
     ids[m * ids_bs + s + 1] = bi;
     bsh = bi;
   }
   __syncthreads();
+  QTX_STAMP(4);
   // next decoder input: tgt_embed(id) at position s + 1 (embeddings.py:12-13)
   if (tid < 128) {
-    const int bi = bsh, p = min(s + 1, max_pos - 1);
+    const int id = bsh;
     const float sc = 0x1.6a09e6p+4f;
-    const float4 e = *reinterpret_cast<const float4*>(lut + (long)bi * 512 + 4 * tid);
-    const float4 q = *reinterpret_cast<const float4*>(pe + (long)p * 512 + 4 * tid);
+    const float4 e = *reinterpret_cast<const float4*>(lut + (long)id * 512 + 4 * tid);
+    const float4 q = pe_row;
     *reinterpret_cast<float4*>(xnext + (long)m * 512 + 4 * tid) =
         make_float4(e.x * sc + q.x, e.y * sc + q.y, e.z * sc + q.z, e.w * sc + q.w);
   }
+  QTX_STAMP(5);
   // every workgroup has read *step above; the last one to arrive advances it
   if (tid == 0) {
     const unsigned tk = atomicAdd(arrive, 1u);
@@ -764,8 +830,8 @@ hipError_t launch_argmax_embed(const float* logits, int M, int V, int64_t* ids, 
                                int max_pos, float* xnext, hipStream_t st) {
   if (M <= 0) return hipSuccess;
   if (V > ARG_MAXV) return hipErrorInvalidValue;
-  k_argmax_embed<<<dim3(M), dim3(256), 0, st>>>(logits, V, ids, ids_bs, step, arrive, lut, pe,
-                                                max_pos, xnext);
+  k_argmax_embed<<<dim3(M), dim3(ARG_T), 0, st>>>(logits, V, ids, ids_bs, step, arrive, lut,
+                                                  pe, max_pos, xnext);
   return hipGetLastError();
 }
 

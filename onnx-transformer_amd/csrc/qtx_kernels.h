@@ -31,38 +31,38 @@ struct GemmArgs {
 enum : int {
   A_I8 = 0,    // int8 A [M,K] + sa[M]
   A_LN = 1,    // fp32 X [M,512]: LayerNorm(ln_a, ln_b) + per-token quant in the prologue
-  A_F32Q = 2,  // fp32 X [M,K] + rowmax bits [M]: quant with s = max(rowmax,1e-5)/127
+  A_F32Q = 2,  // fp32 X [M,K] + partial absmax: quant with s = max(max_p pmax,1e-5)/127
 };
 enum : int {
-  EPI_ROWMAX = 4,  // atomicMax(rowmax_out[m], bits(|y|)) after the other flags
+  EPI_ROWMAX = 4,  // pmax_out[tile][m] = max |y| over the tile's 16 columns (last)
 };
 struct SkinnyArgs {
   int amode;
   const int8_t* A; const float* sa;               // A_I8
   const float* X; long ldx;                       // A_LN / A_F32Q
   const float* ln_a; const float* ln_b;           // A_LN
-  const unsigned* rowmax_in;                      // A_F32Q
+  const float* pmax_in; int pmax_n;               // A_F32Q: [pmax_n][M] partial row absmax
   const int8_t* W; long ldw; const float* sw; const float* bias;
   float* out; long ldo; const float* res; long ldr;
-  unsigned* rowmax_out;                           // EPI_ROWMAX
-  unsigned* zero; int zero_n;                     // block (0,0) zeroes zero[0..n) (side task)
+  float* pmax_out;                                // EPI_ROWMAX: [N/16][M] per column tile
   int M, N, K, flags;
 };
 
-// Fused decode attention: one workgroup (8 waves = 8 heads) per sentence b, one query.
+// Fused decode attention: one wave per (sentence b, head h), one query.
 //   self  (kv_new != 0): q/k/v rows from y [B, 3*512] fp32 are quantized per token;
 //                        k/v appended to the caches at position *step; keys 0..*step.
 //   cross (kv_new == 0): q row from y [B, 512]; keys = the S cached cross K/V rows,
 //                        masked by mask[b*S + j].
-//   Both quantize the context row per token into a8/sa (the next GEMM's A operand).
+//   Both write the fp32 context ctx [B, 512] and the per-head partial absmax
+//   pmax [8][B]; the next GEMM quantizes the row per token from them (A_F32Q).
 struct DecAttnArgs {
   const float* y; long ldy;
   int8_t* kc; int8_t* vc; float* skc; float* svc; long kv_bs;   // [B][kv_bs rows][512]
   const int* step;            // self: current position
   int S;                      // cross: number of keys
   const uint8_t* mask;        // cross: [B, S]
-  int8_t* a8; float* sa;      // out: quantized context [B, 512] + scale
-  int kv_new;
+  float* ctx; float* pmax;    // out
+  int B, kv_new;
 };
 
 // Row quantizer / LayerNorm+quantizer over rows of D floats (one wave per row).

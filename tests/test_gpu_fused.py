@@ -59,6 +59,17 @@ def wdev(torch, qw, bits):
     return wd
 
 
+def tile_max(y):
+    """Per 16-column tile row absmax, [N/16, M] (EPI_ROWMAX output layout)."""
+    M, N = y.shape
+    return np.abs(y).reshape(M, N // 16, 16).max(-1).T
+
+
+def head_max(ctx):
+    """[8, B] per-head absmax of context rows [B, 512]."""
+    return np.abs(ctx).reshape(-1, 8, 64).max(-1).T
+
+
 @pytest.mark.parametrize("M", [1, 2, 16, 32, 45])
 @pytest.mark.parametrize("N,K,flags,bits", [(512, 512, 2, 8), (1536, 512, 0, 8),
                                              (2048, 512, 5, 8), (512, 2048, 2, 4)])
@@ -68,53 +79,57 @@ def test_skinny_i8(torch, M, N, K, flags, bits):
     qw, sw, b = weights(rng, N, K, bits)
     res = rng.standard_normal((M, N)).astype(f32)
     out = dev(torch, res.copy())
-    rm = torch.zeros(M, dtype=torch.int32, device="cuda")
-    call("qtx_skinny_linear", 0, P(dev(torch, qx)), P(dev(torch, sx)), S0, 0, S0, S0, S0,
+    pm = torch.zeros((N // 16, M), dtype=torch.float32, device="cuda")
+    call("qtx_skinny_linear", 0, P(dev(torch, qx)), P(dev(torch, sx)), S0, 0, S0, S0, S0, 0,
          P(wdev(torch, qw, bits)), P(dev(torch, sw)), P(dev(torch, b)), M, N, K, bits, flags,
-         P(out), P(out), P(rm), S0)
+         P(out), P(out), P(pm), S0)
     y = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b, relu=bool(flags & 1))
     if flags & 2:
         y = res + y
     np.testing.assert_array_equal(out.cpu().numpy(), y)
     if flags & 4:
-        np.testing.assert_array_equal(rm.cpu().numpy().view(f32), np.abs(y).max(-1))
+        np.testing.assert_array_equal(pm.cpu().numpy(), tile_max(y))
 
 
-@pytest.mark.parametrize("M", [2, 32])
+@pytest.mark.parametrize("M", [2, 5, 32])
 def test_skinny_layernorm_prologue(torch, M, oracle_model):
     rng = np.random.default_rng(M)
     x = (rng.standard_normal((M, 512)) * 3).astype(f32)
     a, bb = oracle_model.dec[0]["ln"][2]
     qw, sw, b = weights(rng, 2048, 512, 8)
     out = torch.empty((M, 2048), dtype=torch.float32, device="cuda")
-    rm = torch.zeros(M, dtype=torch.int32, device="cuda")
+    pm = torch.zeros((2048 // 16, M), dtype=torch.float32, device="cuda")
     call("qtx_skinny_linear", 1, S0, S0, P(dev(torch, x)), 512, P(dev(torch, a)),
-         P(dev(torch, bb)), S0, P(dev(torch, qw)), P(dev(torch, sw)), P(dev(torch, b)), M,
-         2048, 512, 8, 1 | 4, S0, P(out), P(rm), S0)
+         P(dev(torch, bb)), S0, 0, P(dev(torch, qw)), P(dev(torch, sw)), P(dev(torch, b)), M,
+         2048, 512, 8, 1 | 4, S0, P(out), P(pm), S0)
     qx, sx = O.quant_rows(O.layer_norm(x, a, bb))
     y = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b, relu=True)
     np.testing.assert_array_equal(out.cpu().numpy(), y)
-    np.testing.assert_array_equal(rm.cpu().numpy().view(f32), y.max(-1))
+    np.testing.assert_array_equal(pm.cpu().numpy(), tile_max(y))
 
 
 @pytest.mark.parametrize("M", [3, 32])
-def test_skinny_rowmax_prologue(torch, M):
-    rng = np.random.default_rng(M + 100)
-    h = np.maximum(rng.standard_normal((M, 2048)), 0).astype(f32)
+@pytest.mark.parametrize("K,nparts", [(2048, 128), (512, 8), (512, 1)])
+def test_skinny_partial_max_prologue(torch, M, K, nparts):
+    """amode 2: fp32 rows quantized per token from partial row maxima (FFN2 from FFN1's
+    per-tile maxima; the output projection from the attention's per-head maxima)."""
+    rng = np.random.default_rng(M + K + nparts)
+    h = np.maximum(rng.standard_normal((M, K)), 0).astype(f32)
     h[0] = 0                                         # an all-zero row: clamp 1e-5
-    rowmax = np.abs(h).max(-1).astype(f32)
-    qw, sw, b = weights(rng, 512, 2048, 8)
+    parts = np.abs(h).reshape(M, nparts, K // nparts).max(-1).T.copy()   # [nparts, M]
+    qw, sw, b = weights(rng, 512, K, 8)
     res = rng.standard_normal((M, 512)).astype(f32)
     out = dev(torch, res.copy())
-    call("qtx_skinny_linear", 2, S0, S0, P(dev(torch, h)), 2048, S0, S0,
-         P(dev(torch, rowmax.view(np.uint32))), P(dev(torch, qw)), P(dev(torch, sw)),
-         P(dev(torch, b)), M, 512, 2048, 8, 2, P(out), P(out), S0, S0)
+    call("qtx_skinny_linear", 2, S0, S0, P(dev(torch, h)), K, S0, S0, P(dev(torch, parts)),
+         nparts, P(dev(torch, qw)), P(dev(torch, sw)), P(dev(torch, b)), M, 512, K, 8, 2,
+         P(out), P(out), S0, S0)
     qx, sx = O.quant_rows(h)
     np.testing.assert_array_equal(out.cpu().numpy(),
                                   res + O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b))
 
 
-@pytest.mark.parametrize("B,step,kv_bs", [(2, 0, 8), (3, 5, 8), (32, 40, 72), (1, 127, 128)])
+@pytest.mark.parametrize("B,step,kv_bs", [(2, 0, 8), (3, 5, 8), (32, 40, 72), (1, 127, 128),
+                                          (4, 70, 72), (2, 15, 17)])
 def test_decode_self_attention(torch, B, step, kv_bs):
     rng = np.random.default_rng(B * 1000 + step)
     y = rng.standard_normal((B, 1536)).astype(f32)
@@ -124,10 +139,11 @@ def test_decode_self_attention(torch, B, step, kv_bs):
     svc = rng.uniform(0.002, 0.03, (B, kv_bs)).astype(f32)
     kcd, vcd, skd, svd = dev(torch, kc), dev(torch, vc), dev(torch, skc), dev(torch, svc)
     stepd = dev(torch, np.array([step], np.int32))
-    a8 = torch.empty((B, 512), dtype=torch.int8, device="cuda")
-    sa = torch.empty((B,), dtype=torch.float32, device="cuda")
-    call("qtx_decode_attention", 1, P(dev(torch, y)), 1536, P(kcd), P(vcd), P(skd), P(svd),
-         kv_bs, P(stepd), 0, S0, B, P(a8), P(sa), S0)
+    ctxd = torch.empty((B, 512), dtype=torch.float32, device="cuda")
+    pm = torch.empty((8, B), dtype=torch.float32, device="cuda")
+    for _ in range(2):      # the second call re-appends the same row: idempotent
+        call("qtx_decode_attention", 1, P(dev(torch, y)), 1536, P(kcd), P(vcd), P(skd),
+             P(svd), kv_bs, P(stepd), 0, S0, B, P(ctxd), P(pm), S0)
     qq, sq = O.quant_rows(y[:, :512])
     qk, sk = O.quant_rows(y[:, 512:1024])
     qv, sv = O.quant_rows(y[:, 1024:])
@@ -138,12 +154,11 @@ def test_decode_self_attention(torch, B, step, kv_bs):
     n = step + 1
     ctx, _ = O.attention(qq[:, None], sq[:, None], kc[:, :n], skc[:, :n], vc[:, :n],
                          svc[:, :n], np.ones((B, 1, n), np.uint8))
-    qc, sc = O.quant_rows(ctx[:, 0])
-    np.testing.assert_array_equal(a8.cpu().numpy(), qc)
-    np.testing.assert_array_equal(sa.cpu().numpy(), sc)
+    np.testing.assert_array_equal(ctxd.cpu().numpy(), ctx[:, 0])
+    np.testing.assert_array_equal(pm.cpu().numpy(), head_max(ctx[:, 0]))
 
 
-@pytest.mark.parametrize("B,S", [(2, 16), (32, 72), (5, 128)])
+@pytest.mark.parametrize("B,S", [(2, 16), (32, 72), (5, 128), (3, 1), (2, 17)])
 def test_decode_cross_attention(torch, B, S):
     rng = np.random.default_rng(B + S)
     y = rng.standard_normal((B, 512)).astype(f32)
@@ -154,13 +169,12 @@ def test_decode_cross_attention(torch, B, S):
     mask = np.ones((B, S), np.uint8)
     for b in range(B):
         mask[b, rng.integers(1, S + 1):] = 0
-    a8 = torch.empty((B, 512), dtype=torch.int8, device="cuda")
-    sa = torch.empty((B,), dtype=torch.float32, device="cuda")
+    ctxd = torch.empty((B, 512), dtype=torch.float32, device="cuda")
+    pm = torch.empty((8, B), dtype=torch.float32, device="cuda")
     call("qtx_decode_attention", 0, P(dev(torch, y)), 512, P(dev(torch, kc)), P(dev(torch, vc)),
-         P(dev(torch, skc)), P(dev(torch, svc)), S, S0, S, P(dev(torch, mask)), B, P(a8),
-         P(sa), S0)
+         P(dev(torch, skc)), P(dev(torch, svc)), S, S0, S, P(dev(torch, mask)), B, P(ctxd),
+         P(pm), S0)
     qq, sq = O.quant_rows(y)
     ctx, _ = O.attention(qq[:, None], sq[:, None], kc, skc, vc, svc, mask[:, None])
-    qc, sc = O.quant_rows(ctx[:, 0])
-    np.testing.assert_array_equal(a8.cpu().numpy(), qc)
-    np.testing.assert_array_equal(sa.cpu().numpy(), sc)
+    np.testing.assert_array_equal(ctxd.cpu().numpy(), ctx[:, 0])
+    np.testing.assert_array_equal(pm.cpu().numpy(), head_max(ctx[:, 0]))

@@ -66,7 +66,8 @@ def test_greedy_decode_matches_oracle(torch, gpu_model, oracle_model, golden_mod
 
 @pytest.mark.parametrize("env", [{"QTX_NO_GRAPH": "1"}, {"QTX_UNFUSED": "1"},
                                  {"QTX_GRAPH_STEPS": "13"}, {"QTX_DECODE_GROUPS": "3"},
-                                 {"QTX_DECODE_GROUPS": "2", "QTX_NO_GRAPH": "1"}])
+                                 {"QTX_DECODE_GROUPS": "2", "QTX_NO_GRAPH": "1"},
+                                 {"QTX_SPLIT_LN": "1"}, {"QTX_FFN_QKERNEL": "1"}])
 def test_greedy_paths_agree(torch, gpu_model, monkeypatch, env):
     """The fused+graph decode step, the fused eager step, the unfused kernels, graphs of
     several steps and sub-batches on several streams agree."""

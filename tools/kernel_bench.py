@@ -57,17 +57,20 @@ def main():
     sw = T(np.full(2048, 0.01, np.float32))
     bias = T(np.zeros(2048, np.float32))
     out = torch.empty((B, 2048), device=dev)
-    rm = torch.zeros(B, dtype=torch.int32, device=dev)
     L = _lib.lib()
     res = {}
 
     res["row_quant 2048"] = timeit(lambda st: L.qtx_row_quant(P(h), B, 2048, 127.0, P(q8), P(s8), st))
     res["ln_quant 512"] = timeit(lambda st: L.qtx_layernorm_quant(P(x), P(lna), P(lnb), B, 512, S0, P(q8), P(s8), st))
 
-    def sk(amode, N, K, flags=0):
+    pmi = T(np.full((128, B), 3.0, np.float32))        # partial row maxima (A_F32Q)
+    pmo = torch.empty((128, B), device=dev)
+
+    def sk(amode, N, K, flags=0, nparts=128):
         return lambda st: L.qtx_skinny_linear(amode, P(a8), P(sa), P(x if K == 512 else h), K,
-                                              P(lna), P(lnb), P(rm), P(W[(N, K)]), P(sw), P(bias),
-                                              B, N, K, 8, flags, P(out), P(out), P(rm), st)
+                                              P(lna), P(lnb), P(pmi), nparts, P(W[(N, K)]),
+                                              P(sw), P(bias), B, N, K, 8, flags, P(out), P(out),
+                                              P(pmo), st)
     res["skinny I8 512x512"] = timeit(sk(0, 512, 512))
     res["skinny I8 512x512 +res"] = timeit(sk(0, 512, 512, 2))
     res["skinny I8 1536x512"] = timeit(sk(0, 1536, 512))
@@ -76,6 +79,8 @@ def main():
     res["skinny LN 512x512"] = timeit(sk(1, 512, 512))
     res["skinny LN 2048x512 relu"] = timeit(sk(1, 2048, 512, 1))
     res["skinny F32Q 512x2048"] = timeit(sk(2, 512, 2048, 2))
+    res["skinny F32Q 512x512 +res"] = timeit(sk(2, 512, 512, 2, 8))
+    res["skinny LN 2048x512 relu+pmax"] = timeit(sk(1, 2048, 512, 5))
 
     y = T(rng.standard_normal((B, 1536)).astype(np.float32))
     kc = T(rng.integers(-127, 128, (B, 72, 512)).astype(np.int8))
@@ -84,10 +89,12 @@ def main():
     svc = T(np.full((B, 72), 0.01, np.float32))
     step = T(np.array([40], np.int32))
     mask = T(np.ones((B, 72), np.uint8))
+    ctx = torch.empty((B, 512), device=dev)
+    pma = torch.empty((8, B), device=dev)
     res["dec attn self step40"] = timeit(lambda st: L.qtx_decode_attention(
-        1, P(y), 1536, P(kc), P(vc), P(skc), P(svc), 72, P(step), 0, S0, B, P(a8), P(sa), st))
+        1, P(y), 1536, P(kc), P(vc), P(skc), P(svc), 72, P(step), 0, S0, B, P(ctx), P(pma), st))
     res["dec attn cross S72"] = timeit(lambda st: L.qtx_decode_attention(
-        0, P(y), 512, P(kc), P(vc), P(skc), P(svc), 72, S0, 72, P(mask), B, P(a8), P(sa), st))
+        0, P(y), 512, P(kc), P(vc), P(skc), P(svc), 72, S0, 72, P(mask), B, P(ctx), P(pma), st))
     # generator (+ log_softmax/argmax) through a tiny model handle
     from qtx.model import QtxModel
     from qtx.weights import ModelConfig, synthetic_state_dict

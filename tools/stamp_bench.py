@@ -58,14 +58,16 @@ def main():
     out = torch.empty((B, 2048), device="cuda")
     lna, lnb = T(np.ones(512, np.float32)), T(np.zeros(512, np.float32))
     h = T(np.abs(rng.standard_normal((B, 2048))).astype(np.float32))
-    rm = T(np.full(B, np.float32(3.0)).view(np.int32))
     W2 = T(rng.integers(-127, 128, (512, 2048)).astype(np.int8))
+    ctx = torch.empty((B, 512), device="cuda")
+    pma = torch.empty((8, B), device="cuda")
+    pmi = T(np.full((128, B), 3.0, np.float32))
     cases = {
-        "dec_attn self": (lambda: L.qtx_decode_attention(1, P(y), 1536, P(kc), P(vc), P(skc), P(svc), 72, P(step), 0, S0, B, P(a8), P(sa), S0), B, 5),
-        "dec_attn cross": (lambda: L.qtx_decode_attention(0, P(y), 512, P(kc), P(vc), P(skc), P(svc), 72, S0, 72, P(mask), B, P(a8), P(sa), S0), B, 5),
-        "skinny I8 1536": (lambda: L.qtx_skinny_linear(0, P(a8), P(sa), S0, 512, S0, S0, S0, P(W), P(sw), P(bias), B, 1536, 512, 8, 0, S0, P(out), S0, S0), 96, 4),
-        "skinny LN 1536": (lambda: L.qtx_skinny_linear(1, S0, S0, P(x), 512, P(lna), P(lnb), S0, P(W), P(sw), P(bias), B, 1536, 512, 8, 0, S0, P(out), S0, S0), 96, 4),
-        "skinny F32Q 512x2048": (lambda: L.qtx_skinny_linear(2, S0, S0, P(h), 2048, S0, S0, P(rm), P(W2), P(sw), P(bias), B, 512, 2048, 8, 2, P(out), P(out), S0, S0), 32, 4),
+        "dec_attn self": (lambda: L.qtx_decode_attention(1, P(y), 1536, P(kc), P(vc), P(skc), P(svc), 72, P(step), 0, S0, B, P(ctx), P(pma), S0), 8 * B, 5),
+        "dec_attn cross": (lambda: L.qtx_decode_attention(0, P(y), 512, P(kc), P(vc), P(skc), P(svc), 72, S0, 72, P(mask), B, P(ctx), P(pma), S0), 8 * B, 5),
+        "skinny I8 1536": (lambda: L.qtx_skinny_linear(0, P(a8), P(sa), S0, 512, S0, S0, S0, 0, P(W), P(sw), P(bias), B, 1536, 512, 8, 0, S0, P(out), S0, S0), 96 * B // 8, 4),
+        "skinny LN 1536": (lambda: L.qtx_skinny_linear(1, S0, S0, P(x), 512, P(lna), P(lnb), S0, 0, P(W), P(sw), P(bias), B, 1536, 512, 8, 0, S0, P(out), S0, S0), 96 * B // 4, 4),
+        "skinny F32Q 512x2048": (lambda: L.qtx_skinny_linear(2, S0, S0, P(h), 2048, S0, S0, P(pmi), 128, P(W2), P(sw), P(bias), B, 512, 2048, 8, 2, P(out), P(out), S0, S0), 32 * B // 4, 4),
     }
     for name, (fn, nblk, nst) in cases.items():
         for _ in range(3):
@@ -80,6 +82,24 @@ def main():
               f"block-start spread {start_spread:.0f}  first-start->last-end {total:.0f} cyc "
               f"({total / 2400:.2f} us)")
 
+    # the decode tail: argmax_embed is the last kernel of every step, so after a greedy
+    # decode its stamps (32 blocks, slots 0..5) are the ones left in the buffer
+    from qtx.model import QtxModel
+    from qtx.weights import ModelConfig, synthetic_state_dict
+    m = QtxModel(synthetic_state_dict(1), ModelConfig())
+    src = torch.full((B, 72), 2, dtype=torch.int64, device="cuda")
+    src[:, :40] = 7
+    src[:, 0] = 0
+    src[:, 39] = 1
+    mk = (src != 2).to(torch.uint8)
+    for _ in range(2):
+        buf.zero_()
+        m.greedy(src, mk, max_len=72)
+        torch.cuda.synchronize()
+    st = buf[:B, :6].cpu().numpy().astype(np.float64)
+    print(f"{'argmax_embed':16s} phases(median cyc) {np.median(np.diff(st, axis=1), 0).astype(int).tolist()}")
+
 
 if __name__ == "__main__":
     main()
+
