@@ -50,33 +50,69 @@ def encoder_gemm_ops(B, S, n_layers=6):
     return n_layers * 2 * M * (3 * D * D + D * D + D * F + F * D)
 
 
-def time_kernel_decode_ffn1(model, B, iters=200):
-    """Dominant decode kernel: FFN1 GEMM at M=B (N=2048, K=512) on the model's weights.
-    Returns average duration (s) measured with HIP events on the launch stream."""
+DOMINANT = "k_skinny<1,4,512,8,A_LN,0>"   # LN+QKV GEMM of the decode step (profiles/)
+
+
+def dominant_alg_bytes(B):
+    """Algorithmic bytes of one LN+QKV decode launch: int8 W [1536,512] + fp32 x [B,512] +
+    LN gamma/beta + per-channel scale/bias + fp32 out [B,1536]."""
+    N, K = 3 * D, D
+    return N * K + B * K * 4 + 2 * K * 4 + 2 * N * 4 + B * N * 4
+
+
+def run_dominant(B, iters, stream=None):
+    """Launch the decode step's dominant kernel `iters` times (shapes of the real model:
+    M=B rows, N=1536, K=512, LayerNorm prologue).  Returns (launch fn, keepalive)."""
     import ctypes as C
 
     import torch
 
     from qtx import _lib
     rng = np.random.default_rng(1)
-    a8 = torch.from_numpy(rng.integers(-127, 128, (B, D)).astype(np.int8)).cuda()
-    sa = torch.full((B,), 0.01, device="cuda")
-    out = torch.empty((B, F), device="cuda")
-    w = torch.from_numpy(rng.integers(-127, 128, (F, D)).astype(np.int8)).cuda()
-    sw = torch.full((F,), 0.01, device="cuda")
-    bias = torch.zeros(F, device="cuda")
-    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).cuda()
+    lna = torch.ones(D, device="cuda")
+    lnb = torch.zeros(D, device="cuda")
+    w = torch.from_numpy(rng.integers(-127, 128, (3 * D, D)).astype(np.int8)).cuda()
+    sw = torch.full((3 * D,), 0.01, device="cuda")
+    bias = torch.zeros(3 * D, device="cuda")
+    out = torch.empty((B, 3 * D), device="cuda")
+    st = C.c_void_p(stream if stream is not None else torch.cuda.current_stream().cuda_stream)
     P = lambda t: C.c_void_p(t.data_ptr())
-    args = (P(a8), P(sa), P(w), P(sw), P(bias), B, F, D, 8, 1, C.c_void_p(0), P(out), st)
-    for _ in range(20):
-        _lib.call("qtx_linear_i8", *args)
+    S0 = C.c_void_p(0)
+    args = (1, S0, S0, P(x), D, P(lna), P(lnb), S0, 0, P(w), P(sw), P(bias), B, 3 * D, D, 8, 0,
+            S0, P(out), S0, st)
+
+    def launch():
+        for _ in range(iters):
+            _lib.call("qtx_skinny_linear", *args)
+    return launch, (x, lna, lnb, w, sw, bias, out)
+
+
+def time_dominant(B, iters=200):
+    """Average launch duration (s) of the dominant decode kernel, HIP events on the stream
+    the kernel is launched on (torch's current stream)."""
+    import torch
+    launch, keep = run_dominant(B, 20)
+    launch()
+    launch, keep = run_dominant(B, iters)
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(iters):
-        _lib.call("qtx_linear_i8", *args)
+    launch()
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / 1e3 / iters
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+    (tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_dominant.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        return json.load(f).get("traffic_bytes_per_launch")
 
 
 def cpu_baseline(sd, B=4, S=72, max_len=72, seed=7):
@@ -162,12 +198,12 @@ def main():
     value = tokens / dt
 
     if rank == 0:
-        kt = time_kernel_decode_ffn1(model, B)
-        alg_bytes = F * D + B * D + B * 4 + F * 12 + B * F * 4   # W int8 + A + scales/bias + out f32
-        roof = {"kernel": f"k_gemm FFN1 decode (M={B}, N={F}, K={D}, int8)", "bound": "hbm",
-                "achieved": alg_bytes / kt / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                "frac": alg_bytes / kt / PEAK_HBM, "traffic": None, "avg_us": kt * 1e6,
-                "alg_bytes_per_launch": alg_bytes}
+        kt = time_dominant(B)
+        alg = dominant_alg_bytes(B)
+        roof = {"kernel": f"{DOMINANT}: LN+QKV decode GEMM (M={B}, N={3 * D}, K={D}, int8)",
+                "bound": "hbm", "achieved": alg / kt / 1e9, "peak": PEAK_HBM / 1e9,
+                "unit": "GB/s", "frac": alg / kt / PEAK_HBM, "traffic": pmc_traffic(),
+                "avg_us": kt * 1e6, "alg_bytes_per_launch": alg}
         out = {"metric": "decoded tokens/sec IWSLT14 de-en int8 greedy (batch 32/GPU, 71 steps)",
                "value": value, "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,

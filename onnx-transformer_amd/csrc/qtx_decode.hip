@@ -7,7 +7,8 @@
 //                   per token, appends k/v to the cache, attention; fp32 context + per-head
 //                   absmax for the next GEMM's per-token quantization
 //                   attention.py:23-67, get_quantized_model.py:160-168
-//   k_generator_ln  final LayerNorm fused into the fp32 generator projection  generator.py:14-15
+//   k_generator_mfma final LayerNorm fused into the fp32 generator projection on fp32 MFMA
+//                   generator.py:14-15, decoder.py:16
 //   k_argmax_embed  log_softmax + first argmax + next-token embedding + step advance
 //                   onnx_reference_inference.py:632,640-643
 //
@@ -565,75 +566,6 @@ hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st) {
   }
   if (a.S <= 0 || a.S > DEC_MAXK) return hipErrorInvalidValue;
   return dec_attn_nit<false>(a, B, a.S, st);
-}
-
-// =====================================================================================
-// k_generator_ln: block = 16 vocab rows x 32 token rows (278 blocks for 4444 x 32).
-// The 16 W rows (32 KB) and the 32 x rows are loaded with all loads in flight, the rows
-// are LayerNormed (final norm, decoder.py:16) into LDS, then each thread runs two
-// sequential fma chains over k (the canonical generator order):
-//   logits[m, v] = (fma chain over k of x[m,k] * W[v,k]) + b[v]
-// =====================================================================================
-__global__ __launch_bounds__(256) void k_generator_ln(const float* x, long ldx, int M,
-                                                      const float* ln_a, const float* ln_b,
-                                                      const float* W, const float* bias, int V,
-                                                      float* logits) {
-  __shared__ __attribute__((aligned(16))) float X[32][516];   // +4: rows on distinct banks
-  __shared__ float Wt[512][17];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int v0 = blockIdx.x * 16, m0 = blockIdx.y * 32;
-  float4 wr[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int idx = tid + 256 * j, gv = min(v0 + (idx >> 7), V - 1);
-    wr[j] = *reinterpret_cast<const float4*>(W + (long)gv * 512 + 4 * (idx & 127));
-  }
-  float xv[8][2][4];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int m = min(m0 + wave + 4 * j, M - 1);
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const float4 t = *reinterpret_cast<const float4*>(x + (long)m * ldx + 4 * (lane + 64 * c));
-      xv[j][c][0] = t.x; xv[j][c][1] = t.y; xv[j][c][2] = t.z; xv[j][c][3] = t.w;
-    }
-  }
-  if (ln_a) ln_rows512<8>(xv, ln_a, ln_b, lane);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-      *reinterpret_cast<float4*>(&X[wave + 4 * j][4 * (lane + 64 * c)]) =
-          make_float4(xv[j][c][0], xv[j][c][1], xv[j][c][2], xv[j][c][3]);
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int idx = tid + 256 * j, vv = idx >> 7, k = 4 * (idx & 127);
-    Wt[k][vv] = wr[j].x; Wt[k + 1][vv] = wr[j].y; Wt[k + 2][vv] = wr[j].z; Wt[k + 3][vv] = wr[j].w;
-  }
-  __syncthreads();
-  const int v = tid & 15, mi = tid >> 4;
-  float a0 = 0.0f, a1 = 0.0f;
-#pragma unroll 16
-  for (int k = 0; k < 512; ++k) {
-    const float w = Wt[k][v];
-    a0 = fmaf(X[mi][k], w, a0);
-    a1 = fmaf(X[mi + 16][k], w, a1);
-  }
-  const int gv = v0 + v;
-  if (gv >= V) return;
-  const float bv = bias[gv];
-  if (m0 + mi < M) logits[(long)(m0 + mi) * V + gv] = a0 + bv;
-  if (m0 + mi + 16 < M) logits[(long)(m0 + mi + 16) * V + gv] = a1 + bv;
-}
-
-hipError_t launch_generator_ln(const float* x, long ldx, int M, const float* ln_a,
-                               const float* ln_b, const float* W, const float* b, int V,
-                               float* logits, hipStream_t st) {
-  if (M <= 0) return hipSuccess;
-  k_generator_ln<<<dim3((V + 15) / 16, (M + 31) / 32), dim3(256), 0, st>>>(
-      x, ldx, M, ln_a, ln_b, W, b, V, logits);
-  return hipGetLastError();
 }
 
 // =====================================================================================

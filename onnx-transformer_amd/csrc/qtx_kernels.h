@@ -95,9 +95,6 @@ hipError_t launch_gemm(const GemmArgs& a, int wbits, hipStream_t st);
 hipError_t launch_skinny(const SkinnyArgs& a, int wbits, hipStream_t st);
 hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st);
 // generator with the final LayerNorm fused in (ln_a may be null = no LN)
-hipError_t launch_generator_ln(const float* x, long ldx, int M, const float* ln_a,
-                               const float* ln_b, const float* W, const float* b, int V,
-                               float* logits, hipStream_t st);
 // the same on fp32 MFMA (bit-identical chain); Wt = generator weight transposed [512][V]
 hipError_t launch_generator_mfma(const float* x, long ldx, int M, const float* ln_a,
                                  const float* ln_b, const float* Wt, const float* b, int V,
