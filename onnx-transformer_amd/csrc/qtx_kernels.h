@@ -121,6 +121,8 @@ hipError_t launch_u8_from_any(const void* src, int elem_bytes, long n, uint8_t* 
                               hipStream_t st);
 hipError_t launch_step_inc(int* step, hipStream_t st);
 hipError_t launch_nop(hipStream_t st);
+hipError_t launch_gemm256(const GemmArgs& g, hipStream_t st);
+hipError_t launch_attention_mfma(const AttnArgs& a, hipStream_t st);
 hipError_t launch_fill_col(int64_t* ids, long bs, int B, int64_t val, hipStream_t st);
 
 }  // namespace qtx

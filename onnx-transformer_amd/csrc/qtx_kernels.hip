@@ -10,6 +10,8 @@
 //   k_lsm_argmax    log_softmax + first-index argmax                 onnx_reference_inference.py:640-641
 //
 // Every float step follows the canonical order of qtx_common.h / oracle/qtx_oracle.py.
+#include <cstdlib>
+
 #include "qtx_common.h"
 #include "qtx_kernels.h"
 
@@ -256,6 +258,10 @@ hipError_t launch_gemm(const GemmArgs& g, int wbits, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   if (g.K % 64 != 0 || (wbits != 8 && wbits != 4)) return hipErrorInvalidValue;
   const dim3 block(256);
+  if (wbits == 8 && !getenv("QTX_GEMM128")) {       // QTX_GEMM128: timing experiments only
+    const hipError_t e = launch_gemm256(g, st);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (g.M >= 256) {
     const dim3 grid((g.N + 127) / 128, (g.M + 127) / 128);
     if (wbits == 8) k_gemm<128, 128, 2, 2, 8><<<grid, block, 0, st>>>(g);
@@ -344,6 +350,10 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
   if (a.B <= 0 || a.Sq <= 0) return hipSuccess;
   if (!a.sk_dev && (a.Sk <= 0 || a.Sk > ATT_MAXK)) return hipErrorInvalidValue;
+  if (!getenv("QTX_ATTN_VALU")) {              // QTX_ATTN_VALU: timing experiments only
+    const hipError_t e = launch_attention_mfma(a, st);
+    if (e != hipErrorNotSupported) return e;
+  }
   k_attention<<<dim3(a.H, a.B), dim3(256), 0, st>>>(a);
   return hipGetLastError();
 }

@@ -90,7 +90,8 @@ def test_layernorm_quant(torch, golden_ops, oracle_model, scale):
 @pytest.mark.parametrize("M,N,K,flags,bits", [
     (16, 512, 512, 0, 8), (72, 1536, 512, 0, 8), (300, 512, 512, 2, 8),
     (130, 2048, 512, 1, 8), (257, 512, 2048, 2, 8), (33, 512, 2048, 0, 4),
-    (512, 2048, 512, 1, 4)])
+    (512, 2048, 512, 1, 4), (1000, 1536, 512, 0, 8), (520, 272, 512, 1, 8),
+    (256, 2048, 2048, 3, 8), (300, 512, 640, 2, 8)])
 def test_linear_i8(torch, M, N, K, flags, bits):
     rng = np.random.default_rng(M * N + K)
     x = rng.standard_normal((M, K)).astype(f32)
@@ -113,9 +114,11 @@ def test_linear_i8(torch, M, N, K, flags, bits):
     np.testing.assert_array_equal(out.cpu().numpy(), y)
 
 
-def test_linear_asymmetric_identity(torch):
-    """A = I-like, asymmetric W: catches row/col swaps of the MFMA C layout."""
-    M = N = K = 64 * 2
+@pytest.mark.parametrize("M", [128, 512])
+def test_linear_asymmetric_identity(torch, M):
+    """A = I-like, asymmetric W: catches row/col swaps of the MFMA C layout (both the
+    128x128 and the 256x256 GEMM)."""
+    N = K = M
     qx = np.zeros((M, K), np.int8)
     qx[np.arange(M), np.arange(K)] = 1
     qw = (np.arange(N * K).reshape(N, K) % 251 - 125).astype(np.int8)
