@@ -21,6 +21,8 @@
  *   qtx_layernorm_quant  <- LayerNorm.forward (+ the next W8A8Linear's act quant)
  *                                                            layer_norm.py:12-15
  *   qtx_linear_i8        <- W8A8Linear.forward (int8 GEMM + dequant epilogue) quant_linear.py:111-119
+ *   qtx_linear_rows      <- W8A8Linear.forward + the per-token quantizer / LayerNorm that
+ *                           consumes its output (fused epilogues)        quant_linear.py:111-119
  *   qtx_attention_i8     <- MultiHeadedAttention.attention     attention.py:23-36
  *
  * Conventions: every pointer is a DEVICE pointer (HIP, gfx950) unless the
@@ -137,6 +139,26 @@ int32_t qtx_attention_i8(const int8_t* q, const float* sq, const int8_t* k, cons
                          float* ctx, void* stream);
 
 /* ---- fused decode-step kernels (the KV-cached greedy step is built from these) ---- */
+
+/* Row-complete int8 GEMM (8-bit weights, N % 512 == 0, K % 64 == 0) whose epilogue sees
+ * whole 512-wide row segments; y = ((float(sum_k A W) * sa[m]) * sw[n]) + bias[n]:
+ *   epi 0  per-token quant of y over each 512-column tile t -> out8 + t*o8_ts [M,512]
+ *          (row stride ldo8) and scale os + t*os_ts [M]  (Q/K/V outputs, attention.py:53-56)
+ *   epi 1  (N == 512) x = res + y -> xout; LayerNorm(x; ln_a, ln_b) quantized per token
+ *          -> lnq [M,512] + lns [M], or fp32 -> lnout when lnq is NULL (sublayer_connection.py
+ *          + layer_norm.py of the next sublayer)
+ *   epi 2  relu(y): per-row absmax of each tile -> pmax_out [N/512][M]
+ *   epi 3  relu(y) quantized per token with m = max_p pmax_in[p][M] (p < pmax_n) ->
+ *          out8 [M,N] (ld ldo8) + os [M]         (FFN hidden, position_feed_forward.py:12) */
+typedef struct qtx_row_gemm {
+  const int8_t* A; const float* sa; const int8_t* W; const float* sw; const float* bias;
+  int32_t M, N, K, epi;
+  int8_t* out8; int64_t ldo8, o8_ts; float* os; int64_t os_ts;
+  const float* res; float* xout; const float* ln_a; const float* ln_b;
+  int8_t* lnq; float* lns; float* lnout;
+  float* pmax_out; const float* pmax_in; int32_t pmax_n;
+} qtx_row_gemm;
+int32_t qtx_linear_rows(const qtx_row_gemm* args, void* stream);
 
 /* Skinny int8 GEMM for decode (M small): out = epilogue(A . W^T) with the A operand made
  * in the prologue: amode 0 = int8 A [M,K] + sa; 1 = LayerNorm(X [M,512]; ln_a, ln_b) then

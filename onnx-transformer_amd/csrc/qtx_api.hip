@@ -321,13 +321,16 @@ struct Scratch {
   int8_t* a8;    // [M, F] activation ints (max K)
   float* sa;     // [M]
   float* y;      // [M, max(3D, F)] GEMM output
-  int8_t* q8;    // [M, D]
-  float* sq;     // [M]
-  int8_t* k8;    // [M, D]
+  int8_t* q8;    // [M, D]   q8, k8, v8 contiguous ([3][M][D]) with sq, sk, sv ([3][M]):
+  float* sq;     // [M]      the row GEMM writes the three quantized projections in one
+  int8_t* k8;    // [M, D]   launch (tile stride M*D / M)
   float* sk;
   int8_t* v8;    // [M, D]
   float* sv;
   float* ctx;    // [M, D]
+  int8_t* h8;    // [M, F]  quantized FFN hidden
+  float* sh;     // [M]
+  float* pmax;   // [F/512, M] FFN1 per-tile row maxima
 };
 
 Scratch carve_scratch(Arena& ar, const qtx_config& c, long M) {
@@ -338,10 +341,12 @@ Scratch carve_scratch(Arena& ar, const qtx_config& c, long M) {
   s.a8 = ar.take<int8_t>(M * F);
   s.sa = ar.take<float>(M);
   s.y = ar.take<float>(M * Y);
-  s.q8 = ar.take<int8_t>(M * D); s.sq = ar.take<float>(M);
-  s.k8 = ar.take<int8_t>(M * D); s.sk = ar.take<float>(M);
-  s.v8 = ar.take<int8_t>(M * D); s.sv = ar.take<float>(M);
+  s.q8 = ar.take<int8_t>(3 * M * D); s.k8 = s.q8 + M * D; s.v8 = s.k8 + M * D;
+  s.sq = ar.take<float>(3 * M); s.sk = s.sq + M; s.sv = s.sk + M;
   s.ctx = ar.take<float>(M * D);
+  s.h8 = ar.take<int8_t>(M * F);
+  s.sh = ar.take<float>(M);
+  s.pmax = ar.take<float>((F / 512 + 1) * M);
   return s;
 }
 
@@ -383,6 +388,47 @@ int linear(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa
   g.out = out; g.ldo = ldo; g.res = res; g.ldr = ldo;
   g.M = M; g.N = L.N; g.K = L.K; g.flags = flags;
   HIPCHK(launch_gemm(g, c.weight_bits, st));
+  return QTX_OK;
+}
+
+// Row-complete GEMM (k_gemm_row) for 8-bit weights: epilogues of whole 512-wide rows.
+bool row_path(const qtx_config& c) {
+  return c.weight_bits == 8 && c.d_ff % 512 == 0 && !getenv("QTX_NO_ROWGEMM");
+}
+RowGemmArgs rowgemm(const QLin& L, const int8_t* a8, const float* sa, int M, int epi) {
+  RowGemmArgs g{};
+  g.A = a8; g.lda = L.K; g.sa = sa; g.W = L.q; g.ldw = L.K; g.sw = L.s; g.bias = L.b;
+  g.M = M; g.N = L.N; g.K = L.K; g.epi = epi;
+  return g;
+}
+// out = per-token quantized (a8 . W^T) per 512-wide tile into out8 + t*M*512, os + t*M
+int row_quant(const QLin& L, const int8_t* a8, const float* sa, int M, int8_t* out8,
+              float* os, hipStream_t st) {
+  RowGemmArgs g = rowgemm(L, a8, sa, M, RE_QUANT);
+  g.out8 = out8; g.ldo8 = 512; g.o8_ts = (long)M * 512; g.os = os; g.os_ts = M;
+  HIPCHK(launch_gemm_row(g, st));
+  return QTX_OK;
+}
+// x += a8 . W^T, then LayerNorm(x) (ln) quantized into (lnq, lns) or fp32 into lnout
+int row_res_ln(const QLin& L, const int8_t* a8, const float* sa, int M, float* x,
+               const float* const* ln, int8_t* lnq, float* lns, float* lnout, hipStream_t st) {
+  RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RES_LN);
+  g.res = x; g.xout = x; g.ln_a = ln[0]; g.ln_b = ln[1];
+  g.lnq = lnq; g.lns = lns; g.lnout = lnout;
+  HIPCHK(launch_gemm_row(g, st));
+  return QTX_OK;
+}
+// FFN1: relu(a8 . W1^T) quantized per token over all d_ff columns, two passes (row
+// maxima, then recompute + quantize: cheaper than the fp32 hidden's round trip)
+int row_ffn1(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa, int M,
+             Scratch& s, hipStream_t st) {
+  RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RELU_PMAX);
+  g.pmax_out = s.pmax;
+  HIPCHK(launch_gemm_row(g, st));
+  g.epi = RE_RELU_QUANT_PMAX;
+  g.pmax_in = s.pmax; g.pmax_n = c.d_ff / 512;
+  g.out8 = s.h8; g.ldo8 = c.d_ff; g.os = s.sh;
+  HIPCHK(launch_gemm_row(g, st));
   return QTX_OK;
 }
 
@@ -438,11 +484,33 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
   const qtx_config& c = m->cfg;
   const int D = c.d_model, M = B * S;
   if (x != s.x) HIPCHK(hipMemcpyAsync(s.x, x, (size_t)M * D * 4, hipMemcpyDeviceToDevice, st));
-  for (const EncLayer& L : m->enc) {
-    RC(self_attn_block(c, L.qkv, L.o, L.ln[0], s, B, S, mask, S, 0, st));
-    RC(ffn_block(c, L.w1, L.w2, L.ln[1], s, M, st));
+  if (!row_path(c)) {
+    for (const EncLayer& L : m->enc) {
+      RC(self_attn_block(c, L.qkv, L.o, L.ln[0], s, B, S, mask, S, 0, st));
+      RC(ffn_block(c, L.w1, L.w2, L.ln[1], s, M, st));
+    }
+    RC(ln_out(s.x, M, m->enc_norm, D, out, st));
+    return QTX_OK;
   }
-  RC(ln_out(s.x, M, m->enc_norm, D, out, st));
+  // Every LayerNorm + per-token quantization after the first is fused into the epilogue of
+  // the GEMM that produces the residual it normalizes (O-proj, FFN2); Q/K/V and the FFN
+  // hidden are quantized in their GEMM's epilogue; the last FFN2 applies the final norm.
+  const int NL = c.n_layers;
+  RC(ln_quant(s.x, M, m->enc[0].ln[0], D, s.a8, s.sa, st));
+  for (int l = 0; l < NL; ++l) {
+    const EncLayer& L = m->enc[l];
+    RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st));
+    AttnArgs a = attn_args(s, B, S, S, S);
+    a.mask = mask; a.m_bs = S; a.m_is = 0;
+    HIPCHK(launch_attention(a, st));
+    RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+    RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st));
+    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st));
+    if (l + 1 < NL)
+      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc[l + 1].ln[0], s.a8, s.sa, nullptr, st));
+    else
+      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc_norm, nullptr, nullptr, out, st));
+  }
   return QTX_OK;
 }
 
@@ -467,9 +535,11 @@ CrossKV carve_cross(Arena& ar, const qtx_config& c, long Ms) {
   x.am8 = ar.take<int8_t>(Ms * D);
   x.sam = ar.take<float>(Ms);
   x.y = ar.take<float>(Ms * 2 * D);
-  for (int l = 0; l < c.n_layers; ++l) {
-    x.k8.push_back(ar.take<int8_t>(Ms * D)); x.sk.push_back(ar.take<float>(Ms));
-    x.v8.push_back(ar.take<int8_t>(Ms * D)); x.sv.push_back(ar.take<float>(Ms));
+  for (int l = 0; l < c.n_layers; ++l) {      // k8|v8 and sk|sv contiguous per layer
+    int8_t* kv = ar.take<int8_t>(2 * Ms * D);
+    float* sc = ar.take<float>(2 * Ms);
+    x.k8.push_back(kv); x.v8.push_back(kv + Ms * D);
+    x.sk.push_back(sc); x.sv.push_back(sc + Ms);
   }
   return x;
 }
@@ -480,6 +550,10 @@ int cross_kv(const qtx_model* m, const float* memory, int Ms, CrossKV& x, hipStr
   const int D = c.d_model;
   RC(quant(memory, D, Ms, D, x.am8, x.sam, st));
   for (int l = 0; l < c.n_layers; ++l) {
+    if (row_path(c)) {     // K and V tiles quantized in the GEMM epilogue
+      RC(row_quant(m->dec[l].ckv, x.am8, x.sam, Ms, x.k8[l], x.sk[l], st));
+      continue;
+    }
     RC(linear(c, m->dec[l].ckv, x.am8, x.sam, Ms, 0, nullptr, x.y, 2 * D, st));
     RC(quant(x.y, 2 * D, Ms, D, x.k8[l], x.sk[l], st));
     RC(quant(x.y + D, 2 * D, Ms, D, x.v8[l], x.sv[l], st));
@@ -795,14 +869,42 @@ int32_t qtx_decoder_forward(const qtx_model* m, const float* y, const float* mem
   CrossKV x = carve_cross(ar, c, (long)B * S);
   RC(cross_kv(m, memory, B * S, x, st));
   HIPCHK(hipMemcpyAsync(s.x, y, (size_t)M * D * 4, hipMemcpyDeviceToDevice, st));
-  for (int l = 0; l < c.n_layers; ++l) {
-    const DecLayer& L = m->dec[l];
-    RC(self_attn_block(c, L.qkv, L.o, L.ln[0], s, B, T, tgt_mask,
-                       tgt_mask_batched ? (long)T * T : 0, T, st));
-    RC(cross_attn_block(m, L, l, s, x, B, T, S, src_mask, st));
-    RC(ffn_block(c, L.w1, L.w2, L.ln[2], s, M, st));
+  const long tm_bs = tgt_mask_batched ? (long)T * T : 0;
+  if (!row_path(c)) {
+    for (int l = 0; l < c.n_layers; ++l) {
+      const DecLayer& L = m->dec[l];
+      RC(self_attn_block(c, L.qkv, L.o, L.ln[0], s, B, T, tgt_mask, tm_bs, T, st));
+      RC(cross_attn_block(m, L, l, s, x, B, T, S, src_mask, st));
+      RC(ffn_block(c, L.w1, L.w2, L.ln[2], s, M, st));
+    }
+    RC(ln_out(s.x, M, m->dec_norm, D, out, st));
+    return QTX_OK;
   }
-  RC(ln_out(s.x, M, m->dec_norm, D, out, st));
+  // LayerNorm + quant of each sublayer's input fused into the previous residual GEMM
+  // (as encoder_run); the last FFN2 applies the final decoder norm
+  const int NL = c.n_layers;
+  RC(ln_quant(s.x, M, m->dec[0].ln[0], D, s.a8, s.sa, st));
+  for (int l = 0; l < NL; ++l) {
+    const DecLayer& L = m->dec[l];
+    RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st));
+    AttnArgs a = attn_args(s, B, T, T, T);
+    a.mask = tgt_mask; a.m_bs = tm_bs; a.m_is = T;
+    HIPCHK(launch_attention(a, st));
+    RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+    RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st));
+    RC(row_quant(L.cq, s.a8, s.sa, M, s.q8, s.sq, st));
+    a = attn_args(s, B, T, S, S);
+    a.k = x.k8[l]; a.sk = x.sk[l]; a.v = x.v8[l]; a.sv = x.sv[l];
+    a.mask = src_mask; a.m_bs = S; a.m_is = 0;
+    HIPCHK(launch_attention(a, st));
+    RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+    RC(row_res_ln(L.co, s.a8, s.sa, M, s.x, L.ln[2], s.a8, s.sa, nullptr, st));
+    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st));
+    if (l + 1 < NL)
+      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->dec[l + 1].ln[0], s.a8, s.sa, nullptr, st));
+    else
+      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->dec_norm, nullptr, nullptr, out, st));
+  }
   return QTX_OK;
 }
 
@@ -1004,6 +1106,28 @@ int32_t qtx_linear_i8(const int8_t* A, const float* sa, const void* W, const flo
   g.M = M; g.N = N; g.K = K; g.flags = flags;
   hipError_t e = launch_gemm(g, weight_bits, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "weight_bits=%d", weight_bits);
+  HIPCHK(e);
+  return QTX_OK;
+}
+
+int32_t qtx_linear_rows(const qtx_row_gemm* a, void* stream) {
+  if (!a || !a->A || !a->sa || !a->W || !a->sw || !a->bias) return fail(QTX_E_INVALID, "null argument");
+  RowGemmArgs g{};
+  g.A = a->A; g.lda = a->K; g.sa = a->sa; g.W = a->W; g.ldw = a->K; g.sw = a->sw;
+  g.bias = a->bias; g.M = a->M; g.N = a->N; g.K = a->K; g.epi = a->epi;
+  g.out8 = a->out8; g.ldo8 = a->ldo8; g.o8_ts = a->o8_ts; g.os = a->os; g.os_ts = a->os_ts;
+  g.res = a->res; g.xout = a->xout; g.ln_a = a->ln_a; g.ln_b = a->ln_b;
+  g.lnq = a->lnq; g.lns = a->lns; g.lnout = a->lnout;
+  g.pmax_out = a->pmax_out; g.pmax_in = a->pmax_in; g.pmax_n = a->pmax_n;
+  const bool ok = (g.epi == RE_QUANT && g.out8 && g.os) ||
+                  (g.epi == RE_RES_LN && g.res && g.xout && g.ln_a && g.ln_b &&
+                   (g.lnq ? g.lns != nullptr : g.lnout != nullptr)) ||
+                  (g.epi == RE_RELU_PMAX && g.pmax_out) ||
+                  (g.epi == RE_RELU_QUANT_PMAX && g.out8 && g.os && g.pmax_in && g.pmax_n > 0);
+  if (!ok) return fail(QTX_E_INVALID, "operands missing for epi %d", g.epi);
+  const hipError_t e = launch_gemm_row(g, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue)
+    return fail(QTX_E_UNSUPPORTED, "rows GEMM: N=%d K=%d epi=%d", g.N, g.K, g.epi);
   HIPCHK(e);
   return QTX_OK;
 }

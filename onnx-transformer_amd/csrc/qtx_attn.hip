@@ -17,6 +17,8 @@
 #include "qtx_common.h"
 #include "qtx_kernels.h"
 
+QTX_STAMP_SETTER(attn)
+
 namespace qtx {
 
 constexpr int AM_MAXK = 128;
@@ -37,19 +39,38 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   const int Sk = a.Sk, Sq = a.Sq, hoff = h * 64;
   const int nk4 = (Sk + 3) & ~3;            // keys rounded up to the MFMA k step
   const int r0 = blockIdx.z * 64 + wave * 16;
+  QTX_STAMP(0);
 
   // ---- stage K, V (rows < nk4; rows >= Sk zero) and the key scales -------------------
   const int8_t* kb = a.k + b * a.k_bs + hoff;
   const int8_t* vb = a.v + b * a.v_bs + hoff;
-  for (int idx = tid; idx < nk4 * 4; idx += 256) {       // 4 x 16 B per 64-byte row
-    const int j = idx >> 2, c = idx & 3;
-    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-    if (j < Sk) {
-      kv = *reinterpret_cast<const uint4*>(kb + (long)j * a.k_ld + 16 * c);
-      vv = *reinterpret_cast<const uint4*>(vb + (long)j * a.v_ld + 16 * c);
+  if (tid < nk4) {        // thread j stages key row j: K swizzled, V transposed (below)
+    const int j = tid, jc = min(j, Sk - 1);
+    const bool ok = j < Sk;
+    uint4 kv[4], vv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {          // clamped, unconditional loads; zeroed if j >= Sk
+      kv[c] = *reinterpret_cast<const uint4*>(kb + (long)jc * a.k_ld + 16 * c);
+      vv[c] = *reinterpret_cast<const uint4*>(vb + (long)jc * a.v_ld + 16 * c);
     }
-    *reinterpret_cast<uint4*>(Ks + j * 64 + 16 * am_slot(j, c)) = kv;
-    *reinterpret_cast<uint4*>(Vs + j * 64 + 16 * c) = vv;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      *reinterpret_cast<uint4*>(Ks + j * 64 + 16 * am_slot(j, c)) = ok ? kv[c] : make_uint4(0, 0, 0, 0);
+    // Vt dword (j, f) = bytes v[j][f], v[j][16+f], v[j][32+f], v[j][48+f] (f = 0..15): the PV
+    // B operand of lane (f = lane & 15) for the four 16-wide dim tiles in one ds_read_b32
+    uint32_t* vt = reinterpret_cast<uint32_t*>(Vs + j * 64);
+    const uint32_t* w0 = reinterpret_cast<const uint32_t*>(&vv[0]);
+    const uint32_t* w1 = reinterpret_cast<const uint32_t*>(&vv[1]);
+    const uint32_t* w2 = reinterpret_cast<const uint32_t*>(&vv[2]);
+    const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&vv[3]);
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+      const int q = f >> 2, pb = f & 3;
+      const uint32_t sel = (uint32_t)pb | ((uint32_t)(pb + 4) << 8);   // [lo.pb, hi.pb]
+      const uint32_t t01 = __builtin_amdgcn_perm(w1[q], w0[q], sel);
+      const uint32_t t23 = __builtin_amdgcn_perm(w3[q], w2[q], sel);
+      vt[f] = ok ? __builtin_amdgcn_perm(t23, t01, 0x05040100u) : 0u;
+    }
   }
   const bool row_mask = a.mask && a.m_is != 0;   // per-query mask rows (causal decoder)
   for (int j = tid; j < nk4; j += 256) {
@@ -65,6 +86,7 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   for (int e = 0; e < 4; ++e) sqr[e] = a.sq[b * a.sq_bs + min(r0 + 4 * fg + e, Sq - 1)];
   __syncthreads();
   if (r0 >= Sq) return;                    // (after the only block-wide barrier)
+  QTX_STAMP(1);
 
   // ---- scores: one i8 MFMA per 16 keys ---------------------------------------------------
   float* P = Pl[wave];
@@ -88,32 +110,67 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   }
   __builtin_amdgcn_wave_barrier();
 
-  // ---- softmax per row (canonical: lane l owns keys l, l+64), P quantized to 1/127 -------
-  for (int row = 0; row < 16; ++row) {
-    float* pr = P + row * AM_PS;
-    const bool v0 = lane < Sk, v1 = lane + 64 < Sk;
-    const float x0 = v0 ? pr[lane] : -3.0e38f, x1 = v1 ? pr[lane + 64] : -3.0e38f;
-    const float m = wave_max(fmaxf(x0, x1));
-    const float e0 = v0 ? qexp(x0 - m) : 0.0f, e1 = v1 ? qexp(x1 - m) : 0.0f;
-    float ls = 0.0f;
-    if (v0) ls = ls + e0;
-    if (v1) ls = ls + e1;
-    const float den = wave_sum(ls);
-    // keys in [Sk, nk4) get P = 0: the padded MFMA k steps then add exact zeros
-    if (lane < nk4) pr[lane] = v0 ? rintf((e0 / den) * 127.0f) / 127.0f : 0.0f;
-    if (lane + 64 < nk4) pr[lane + 64] = v1 ? rintf((e1 / den) * 127.0f) / 127.0f : 0.0f;
+  QTX_STAMP(2);
+  // ---- softmax, 4 rows per pass: the 16-lane DPP row r of the wave holds query row rb+r,
+  // lane j of it keys j + 16 i (i < 8).  Canonical order: lane-split partial of position L
+  // (L < 64) = (0 + e[L]) + e[L+64]; positions j, j+16, j+32, j+48 live in lane j, so the
+  // 64-position pairwise tree = a 16-lane tree per register, then (S0 + S1) + (S2 + S3).
+  {
+    const int sub = lane >> 4, jj = lane & 15;
+    for (int rb = 0; rb < 16; rb += 4) {
+      float* pr = P + (rb + sub) * AM_PS;
+      float x[8], e[8];
+      float m = -3.0e38f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int key = jj + 16 * i;
+        x[i] = key < Sk ? pr[key] : -3.0e38f;
+        m = fmaxf(m, x[i]);
+      }
+      m = row16_max(m);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e[i] = (jj + 16 * i < Sk) ? qexp(x[i] - m) : 0.0f;
+      float pp[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pp[q] = row16_sum((0.0f + e[q]) + e[q + 4]);
+      const float den = (pp[0] + pp[1]) + (pp[2] + pp[3]);
+      // e/den correctly rounded via the shared reciprocal (div_cr) unless some e is outside
+      // its range (then the true division, wave-uniform); q/127 likewise (always in range)
+      DivRange rg;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rg.add(e[i]);
+      const bool fast = __ballot(!(rg.ok() && divisor_ok(den))) == 0ull;
+      const float rden = 1.0f / den, r127 = 1.0f / 127.0f;
+      float p[8];
+      if (fast) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) p[i] = div_cr(e[i], den, rden);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) p[i] = e[i] / den;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int key = jj + 16 * i;      // keys in [Sk, nk4) get P = 0 (padded MFMA steps)
+        const float pq = div_cr(rintf(p[i] * 127.0f), 127.0f, r127);
+        if (key < nk4) pr[key] = key < Sk ? pq : 0.0f;
+      }
+    }
   }
   __builtin_amdgcn_wave_barrier();
-
+  QTX_STAMP(3);
   // ---- PV on fp32 MFMA: A = P[row fr][k], B = float(v[k][d]) * s_v[k], k = 4s + fg -------
   v4f acc[4] = {v4f{0, 0, 0, 0}, v4f{0, 0, 0, 0}, v4f{0, 0, 0, 0}, v4f{0, 0, 0, 0}};
+  const uint32_t* vt32 = reinterpret_cast<const uint32_t*>(Vs);
+#pragma unroll 4
   for (int s = 0; s < nk4 / 4; ++s) {
     const int k = 4 * s + fg;
     const float pa = P[fr * AM_PS + k];
     const float svk = svs[k];
+    const uint32_t vd = vt32[k * 16 + fr];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      const float vb2 = (float)Vs[k * 64 + dt * 16 + fr] * svk;
+      const float vb2 = (float)(int8_t)(vd >> (8 * dt)) * svk;
       acc[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa, vb2, acc[dt], 0, 0, 0);
     }
   }
@@ -124,6 +181,7 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
       const int row = r0 + 4 * fg + e;
       if (row < Sq) a.ctx[b * a.c_bs + (long)row * a.c_ld + hoff + dt * 16 + fr] = acc[dt][e];
     }
+  QTX_STAMP(4);
 }
 
 // Returns hipErrorNotSupported for shapes it does not take (caller keeps k_attention).

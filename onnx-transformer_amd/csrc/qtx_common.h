@@ -19,6 +19,13 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // with -DQTX_STAMPS; thread 0 of each block records s_memtime at phase boundaries into
 // qtx_stamp_buf[block][slot] (a device buffer of its own; never read by the kernels).
 #ifdef QTX_STAMPS
+// one buffer pointer per translation unit; each .hip that stamps exports a setter
+// qtx_debug_set_stamps_<unit> (QTX_STAMP_SETTER below)
+static __device__ unsigned long long* qtx_stamp_buf;
+#define QTX_STAMP_SETTER(unit)                                                            \
+  extern "C" int qtx_debug_set_stamps_##unit(void* buf) {                                 \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(qtx_stamp_buf), &buf, sizeof(buf));          \
+  }
 #define QTX_STAMP(slot)                                                                 \
   do {                                                                                    \
     if (threadIdx.x == 0 && qtx_stamp_buf)                                                \
@@ -26,6 +33,7 @@ typedef float v4f __attribute__((ext_vector_type(4)));
           __builtin_amdgcn_s_memtime();                                                   \
   } while (0)
 #else
+#define QTX_STAMP_SETTER(unit)
 #define QTX_STAMP(slot) \
   do {                  \
   } while (0)
@@ -62,6 +70,21 @@ __device__ __forceinline__ float wave_max(float v) {
   v = fmaxf(v, dpp<0x141>(v));
   v = fmaxf(v, dpp<0x140>(v));
   return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
+}
+
+// The same trees restricted to each 16-lane DPP row: every lane of the row gets the row's
+// canonical sum / max (the first four levels of wave_sum).
+__device__ __forceinline__ float row16_sum(float v) {
+  v = v + dpp<0xB1>(v);
+  v = v + dpp<0x4E>(v);
+  v = v + dpp<0x141>(v);
+  return v + dpp<0x140>(v);
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  return fmaxf(v, dpp<0x140>(v));
 }
 
 __device__ __forceinline__ int wave_min_i32(int v) {
@@ -180,5 +203,102 @@ __device__ __forceinline__ int quant_one(float x, float s) {
 
 // |x| as an order-preserving uint (for atomicMax on non-negative floats)
 __device__ __forceinline__ unsigned abs_bits(float x) { return __float_as_uint(fabsf(x)); }
+
+// LayerNorm (canonical order, layer_norm.py:12-15) of R rows of 512 floats, each held as
+// 2 float4 per lane, in place.  The R rows are processed step by step together so their
+// independent reduction chains overlap (ILP) instead of running one row after another.
+template <int R>
+__device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float* a, const float* b,
+                                           int lane) {
+  float mean[R], den[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    float s = v[j][0][0];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (c | e) s = s + v[j][c][e];
+    mean[j] = s;
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) mean[j] = wave_sum(mean[j]) / 512.0f;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][c][e] = v[j][c][e] - mean[j];   // v now holds d
+    float ss = v[j][0][0] * v[j][0][0];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (c | e) ss = ss + v[j][c][e] * v[j][c][e];
+    den[j] = ss;
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) den[j] = sqrtf(wave_sum(den[j]) / 511.0f) + 1e-6f;
+  // y = (a * d) / den + b, the division correctly rounded via div_cr (one true division
+  // per row for the reciprocal), true division if any value is outside div_cr's range
+  float ga[2][4], gb[2][4];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float4 ta = *reinterpret_cast<const float4*>(a + 4 * (lane + 64 * c));
+    const float4 tb = *reinterpret_cast<const float4*>(b + 4 * (lane + 64 * c));
+    ga[c][0] = ta.x; ga[c][1] = ta.y; ga[c][2] = ta.z; ga[c][3] = ta.w;
+    gb[c][0] = tb.x; gb[c][1] = tb.y; gb[c][2] = tb.z; gb[c][3] = tb.w;
+  }
+  DivRange rg;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[j][c][e] = ga[c][e] * v[j][c][e];     // numerator a * d
+        rg.add(v[j][c][e]);
+      }
+  }
+  bool ok = rg.ok();
+#pragma unroll
+  for (int j = 0; j < R; ++j) ok &= divisor_ok(den[j]);
+  if (__builtin_expect(__ballot(!ok) == 0ull, 1)) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const float y = 1.0f / den[j];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[j][c][e] = div_cr(v[j][c][e], den[j], y) + gb[c][e];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[j][c][e] = v[j][c][e] / den[j] + gb[c][e];
+  }
+}
+
+// per-token quantization of R rows (2 float4 per lane each) into int8 dwords + scales
+template <int R>
+__device__ __forceinline__ void quant_rows512(const float (&v)[R][2][4], uint32_t (&q)[R][2],
+                                              float (&sc)[R]) {
+  float am[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    am[j] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) am[j] = fmaxf(am[j], fabsf(v[j][c][e]));
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) sc[j] = quant_scale(wave_max(am[j]), 127.0f);
+#pragma unroll
+  for (int j = 0; j < R; ++j) quant_pack<8>(&v[j][0][0], sc[j], q[j]);
+}
 
 }  // namespace qtx

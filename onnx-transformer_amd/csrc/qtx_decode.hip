@@ -18,12 +18,7 @@
 #include "qtx_common.h"
 #include "qtx_kernels.h"
 
-#ifdef QTX_STAMPS
-__device__ unsigned long long* qtx_stamp_buf;
-extern "C" int qtx_debug_set_stamps(void* buf) {
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(qtx_stamp_buf), &buf, sizeof(buf));
-}
-#endif
+QTX_STAMP_SETTER(decode)
 
 namespace qtx {
 
@@ -37,103 +32,6 @@ __device__ __forceinline__ uint4 unpack_i4(uint2 h) {
   o.z = __builtin_amdgcn_perm(hi1, lo1, 0x05010400u);
   o.w = __builtin_amdgcn_perm(hi1, lo1, 0x07030602u);
   return o;
-}
-
-// LayerNorm (canonical order, layer_norm.py:12-15) of R rows of 512 floats, each held as
-// 2 float4 per lane, in place.  The R rows are processed step by step together so their
-// independent reduction chains overlap (ILP) instead of running one row after another.
-template <int R>
-__device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float* a, const float* b,
-                                           int lane) {
-  float mean[R], den[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    float s = v[j][0][0];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (c | e) s = s + v[j][c][e];
-    mean[j] = s;
-  }
-#pragma unroll
-  for (int j = 0; j < R; ++j) mean[j] = wave_sum(mean[j]) / 512.0f;
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[j][c][e] = v[j][c][e] - mean[j];   // v now holds d
-    float ss = v[j][0][0] * v[j][0][0];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (c | e) ss = ss + v[j][c][e] * v[j][c][e];
-    den[j] = ss;
-  }
-#pragma unroll
-  for (int j = 0; j < R; ++j) den[j] = sqrtf(wave_sum(den[j]) / 511.0f) + 1e-6f;
-  // y = (a * d) / den + b, the division correctly rounded via div_cr (one true division
-  // per row for the reciprocal), true division if any value is outside div_cr's range
-  float ga[2][4], gb[2][4];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const float4 ta = *reinterpret_cast<const float4*>(a + 4 * (lane + 64 * c));
-    const float4 tb = *reinterpret_cast<const float4*>(b + 4 * (lane + 64 * c));
-    ga[c][0] = ta.x; ga[c][1] = ta.y; ga[c][2] = ta.z; ga[c][3] = ta.w;
-    gb[c][0] = tb.x; gb[c][1] = tb.y; gb[c][2] = tb.z; gb[c][3] = tb.w;
-  }
-  DivRange rg;
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[j][c][e] = ga[c][e] * v[j][c][e];     // numerator a * d
-        rg.add(v[j][c][e]);
-      }
-  }
-  bool ok = rg.ok();
-#pragma unroll
-  for (int j = 0; j < R; ++j) ok &= divisor_ok(den[j]);
-  if (__builtin_expect(__ballot(!ok) == 0ull, 1)) {
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const float y = 1.0f / den[j];
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[j][c][e] = div_cr(v[j][c][e], den[j], y) + gb[c][e];
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < R; ++j)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[j][c][e] = v[j][c][e] / den[j] + gb[c][e];
-  }
-}
-
-// per-token quantization of R rows (2 float4 per lane each) into int8 dwords + scales
-template <int R>
-__device__ __forceinline__ void quant_rows512(const float (&v)[R][2][4], uint32_t (&q)[R][2],
-                                              float (&sc)[R]) {
-  float am[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    am[j] = 0.0f;
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) am[j] = fmaxf(am[j], fabsf(v[j][c][e]));
-  }
-#pragma unroll
-  for (int j = 0; j < R; ++j) sc[j] = quant_scale(wave_max(am[j]), 127.0f);
-#pragma unroll
-  for (int j = 0; j < R; ++j) quant_pack<8>(&v[j][0][0], sc[j], q[j]);
 }
 
 // =====================================================================================

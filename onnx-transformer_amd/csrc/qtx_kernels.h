@@ -91,6 +91,28 @@ struct AttnArgs {
   const int* qpos_dev;                      // if set, query i's mask row = *qpos_dev + i
 };
 
+// Row-complete int8 GEMM (large M, 8-bit weights, N % 512 == 0, K % 64 == 0): each
+// workgroup owns 128 rows x one 512-wide column tile, so epilogues that need a whole
+// 512-wide row segment run in the same kernel.  y = ((float(acc) * sa[m]) * sw[n]) + b[n]:
+//   RE_QUANT            per-token quant of y over the tile -> out8 + t*o8_ts [M,512] (ld
+//                       ldo8) and scale os + t*os_ts [M]        (Q/K/V outputs, cross K/V)
+//   RE_RES_LN           x = res + y -> xout [M,512]; LayerNorm(x) (ln_a, ln_b) quantized per
+//                       token -> lnq [M,512] + lns [M], or fp32 -> lnout   (O-proj / FFN2)
+//   RE_RELU_PMAX        relu(y): per-row absmax of the tile -> pmax_out [N/512][M] (no y)
+//   RE_RELU_QUANT_PMAX  relu(y) quantized per token with the max over pmax_in [pmax_n][M]
+//                       -> out8 [M,N] (ld ldo8) + os [M]                 (FFN1, 2nd pass)
+enum RowEpi { RE_QUANT = 0, RE_RES_LN = 1, RE_RELU_PMAX = 2, RE_RELU_QUANT_PMAX = 3 };
+struct RowGemmArgs {
+  const int8_t* A; long lda; const float* sa;
+  const int8_t* W; long ldw; const float* sw; const float* bias;
+  int M, N, K, epi;
+  int8_t* out8; long ldo8, o8_ts; float* os; long os_ts;
+  const float* res; float* xout; const float* ln_a; const float* ln_b;
+  int8_t* lnq; float* lns; float* lnout;
+  float* pmax_out; const float* pmax_in; int pmax_n;
+};
+hipError_t launch_gemm_row(const RowGemmArgs& a, hipStream_t st);
+
 hipError_t launch_gemm(const GemmArgs& a, int wbits, hipStream_t st);
 hipError_t launch_skinny(const SkinnyArgs& a, int wbits, hipStream_t st);
 hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st);

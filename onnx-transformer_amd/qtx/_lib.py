@@ -31,6 +31,16 @@ class QtxConfig(C.Structure):
 P = C.c_void_p
 I32, I64, SZ, F32 = C.c_int32, C.c_int64, C.c_size_t, C.c_float
 
+
+class RowGemm(C.Structure):
+    """struct qtx_row_gemm (include/qtx.h)."""
+    _fields_ = [("A", P), ("sa", P), ("W", P), ("sw", P), ("bias", P),
+                ("M", I32), ("N", I32), ("K", I32), ("epi", I32),
+                ("out8", P), ("ldo8", I64), ("o8_ts", I64), ("os", P), ("os_ts", I64),
+                ("res", P), ("xout", P), ("ln_a", P), ("ln_b", P),
+                ("lnq", P), ("lns", P), ("lnout", P),
+                ("pmax_out", P), ("pmax_in", P), ("pmax_n", I32)]
+
 # name -> (restype, argtypes); must match include/qtx.h
 SIGNATURES = {
     "qtx_last_error": (C.c_char_p, []),
@@ -50,6 +60,7 @@ SIGNATURES = {
     "qtx_row_quant": (I32, [P, I32, I32, F32, P, P, P]),
     "qtx_layernorm_quant": (I32, [P, P, P, I32, I32, P, P, P, P]),
     "qtx_linear_i8": (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, P, P, P]),
+    "qtx_linear_rows": (I32, [C.POINTER(RowGemm), P]),
     "qtx_pack_int4": (I32, [P, I32, I32, P, P]),
     "qtx_attention_i8": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, P]),
     "qtx_skinny_linear": (I32, [I32, P, P, P, I64, P, P, P, I32, P, P, P, I32, I32, I32, I32,

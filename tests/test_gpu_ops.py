@@ -175,3 +175,85 @@ def test_generator(torch, gpu_model, golden_ops, oracle_model):
     lo, io = oracle_model.generator(x)
     np.testing.assert_array_equal(ids.cpu().numpy(), io)
     assert np.abs(logp.cpu().numpy() - lo).max() <= 2e-6
+
+
+def _rows_call(torch, **kw):
+    from qtx._lib import RowGemm, lib
+    import ctypes as C
+    a = RowGemm()
+    for k, v in kw.items():
+        setattr(a, k, v.data_ptr() if hasattr(v, "data_ptr") else v)
+    rc = lib().qtx_linear_rows(C.byref(a), S0)
+    assert rc == 0, lib().qtx_last_error()
+
+
+@pytest.mark.parametrize("M", [300, 128, 7])
+def test_linear_rows_quant_qkv(torch, M):
+    """epi 0: Q/K/V GEMM with the per-token output quantization of each 512-wide tile."""
+    rng = np.random.default_rng(M + 1)
+    qx, sx = O.quant_rows(rng.standard_normal((M, 512)).astype(f32))
+    qw, sw = O.quant_weight((rng.standard_normal((1536, 512)) * 0.05).astype(f32), 8)
+    b = rng.standard_normal(1536).astype(f32)
+    out8 = torch.empty((3, M, 512), dtype=torch.int8, device="cuda")
+    os_ = torch.empty((3, M), dtype=torch.float32, device="cuda")
+    _rows_call(torch, A=dev(torch, qx), sa=dev(torch, sx), W=dev(torch, qw), sw=dev(torch, sw),
+               bias=dev(torch, b), M=M, N=1536, K=512, epi=0, out8=out8, ldo8=512,
+               o8_ts=M * 512, os=os_, os_ts=M)
+    y = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b)
+    for t in range(3):
+        q, s = O.quant_rows(y[:, 512 * t:512 * (t + 1)])
+        np.testing.assert_array_equal(out8[t].cpu().numpy(), q)
+        np.testing.assert_array_equal(os_[t].cpu().numpy(), s)
+
+
+@pytest.mark.parametrize("M,K,quant", [(300, 2048, True), (130, 512, False), (5, 512, True)])
+def test_linear_rows_residual_layernorm(torch, oracle_model, M, K, quant):
+    """epi 1: x = res + y, then the next sublayer's LayerNorm (+ per-token quant)."""
+    rng = np.random.default_rng(M + K)
+    qx, sx = O.quant_rows(rng.standard_normal((M, K)).astype(f32))
+    qw, sw = O.quant_weight((rng.standard_normal((512, K)) * 0.05).astype(f32), 8)
+    b = rng.standard_normal(512).astype(f32)
+    res = (rng.standard_normal((M, 512)) * 2).astype(f32)
+    la, lb = oracle_model.dec[1]["ln"][0]
+    xd = dev(torch, res.copy())
+    kw = dict(A=dev(torch, qx), sa=dev(torch, sx), W=dev(torch, qw), sw=dev(torch, sw),
+              bias=dev(torch, b), M=M, N=512, K=K, epi=1, res=xd, xout=xd,
+              ln_a=dev(torch, la), ln_b=dev(torch, lb))
+    if quant:
+        lnq = torch.empty((M, 512), dtype=torch.int8, device="cuda")
+        lns = torch.empty(M, dtype=torch.float32, device="cuda")
+        kw.update(lnq=lnq, lns=lns)
+    else:
+        lnout = torch.empty((M, 512), dtype=torch.float32, device="cuda")
+        kw.update(lnout=lnout)
+    _rows_call(torch, **kw)
+    x = res + O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b)
+    np.testing.assert_array_equal(xd.cpu().numpy(), x)
+    ln = O.layer_norm(x, la, lb)
+    if quant:
+        q, s = O.quant_rows(ln)
+        np.testing.assert_array_equal(lnq.cpu().numpy(), q)
+        np.testing.assert_array_equal(lns.cpu().numpy(), s)
+    else:
+        np.testing.assert_array_equal(lnout.cpu().numpy(), ln)
+
+
+@pytest.mark.parametrize("M", [260, 33])
+def test_linear_rows_ffn1_two_pass(torch, M):
+    """epi 2 + 3: relu(FFN1) tile maxima, then recompute + per-token quant over d_ff."""
+    rng = np.random.default_rng(M + 7)
+    qx, sx = O.quant_rows(rng.standard_normal((M, 512)).astype(f32))
+    qw, sw = O.quant_weight((rng.standard_normal((2048, 512)) * 0.05).astype(f32), 8)
+    b = rng.standard_normal(2048).astype(f32)
+    pm = torch.empty((4, M), dtype=torch.float32, device="cuda")
+    base = dict(A=dev(torch, qx), sa=dev(torch, sx), W=dev(torch, qw), sw=dev(torch, sw),
+                bias=dev(torch, b), M=M, N=2048, K=512)
+    _rows_call(torch, epi=2, pmax_out=pm, **base)
+    h = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b, relu=True)
+    np.testing.assert_array_equal(pm.cpu().numpy(), h.reshape(M, 4, 512).max(-1).T)
+    h8 = torch.empty((M, 2048), dtype=torch.int8, device="cuda")
+    sh = torch.empty(M, dtype=torch.float32, device="cuda")
+    _rows_call(torch, epi=3, pmax_in=pm, pmax_n=4, out8=h8, ldo8=2048, os=sh, **base)
+    q, s = O.quant_rows(h)
+    np.testing.assert_array_equal(h8.cpu().numpy(), q)
+    np.testing.assert_array_equal(sh.cpu().numpy(), s)

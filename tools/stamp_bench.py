@@ -36,7 +36,8 @@ def main():
     L = _lib.lib(build=False)
     raw = C.CDLL(STAMP_LIB)
     buf = torch.zeros((4096, 16), dtype=torch.int64, device="cuda")
-    raw.qtx_debug_set_stamps(C.c_void_p(buf.data_ptr()))
+    for unit in ("decode", "attn"):
+        getattr(raw, f"qtx_debug_set_stamps_{unit}")(C.c_void_p(buf.data_ptr()))
     P = lambda t: C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
     S0 = C.c_void_p(0)
     B = 32
@@ -62,7 +63,13 @@ def main():
     ctx = torch.empty((B, 512), device="cuda")
     pma = torch.empty((8, B), device="cuda")
     pmi = T(np.full((128, B), 3.0, np.float32))
+    Be, Se = 256, 128                       # cfg3 encoder attention
+    qe = T(rng.integers(-127, 128, (Be, Se, 512)).astype(np.int8))
+    se = T(np.full((Be, Se), 0.01, np.float32))
+    me = T(np.ones((Be, Se), np.uint8))
+    ce = torch.empty((Be, Se, 512), device="cuda")
     cases = {
+        "attn_mfma cfg3": (lambda: L.qtx_attention_i8(P(qe), P(se), P(qe), P(se), P(qe), P(se), P(me), Se, 0, Be, 8, Se, Se, P(ce), S0), 8 * Be, 5),
         "dec_attn self": (lambda: L.qtx_decode_attention(1, P(y), 1536, P(kc), P(vc), P(skc), P(svc), 72, P(step), 0, S0, B, P(ctx), P(pma), S0), 8 * B, 5),
         "dec_attn cross": (lambda: L.qtx_decode_attention(0, P(y), 512, P(kc), P(vc), P(skc), P(svc), 72, S0, 72, P(mask), B, P(ctx), P(pma), S0), 8 * B, 5),
         "skinny I8 1536": (lambda: L.qtx_skinny_linear(0, P(a8), P(sa), S0, 512, S0, S0, S0, 0, P(W), P(sw), P(bias), B, 1536, 512, 8, 0, S0, P(out), S0, S0), 96 * B // 8, 4),
