@@ -8,12 +8,21 @@
 // The PV chain runs on v_mfma_f32_16x16x4f32: chained over k in order (C starts at 0) it
 // is bit-for-bit the k-ordered fmaf chain (the generator relies on the same fact), so the
 // canonical sequential-fma PV becomes 16x16 tiles on the matrix cores instead of one
-// latency-bound VALU chain per (row, dim).  Softmax rows use the canonical lane-split sum.
+// latency-bound VALU chain per (row, dim).
 //
 // k_attn_mfma: workgroup = (head h, sentence b, block of 64 query rows), 4 waves, wave w
 // owns query rows 16w..16w+15 of the block.  K and V (int8, per head) and their scales
-// are staged in LDS once per workgroup; the scores / P of a wave's 16 rows live in LDS.
-// Keys <= 128.
+// are staged in LDS once per workgroup.  Everything after that stays in registers:
+// the scores are computed TRANSPOSED (S^T = K Q^T: A = 16 keys, B = the wave's 16 query
+// rows) from K rows staged in the key order perm(j) (the two 2-bit fields of j & 15
+// swapped), so C row 4 fg + e of key tile kt is key 16 kt + 4 e + fg: lane (fr, fg) holds
+// row i = fr at keys 4 s + fg (s = 4 kt + e) — exactly the A operand of step s of the PV
+// MFMA chain (row fr, k = 4 s + fg).
+// Softmax reductions: 32 values in the lane, then lanes xor 16 / xor 32 (permlane swaps).
+// The canonical denominator tree (oracle row_sum_lanesplit: lane-split partial of
+// position L = (0 + e[L]) + e[L+64], then a 64-position xor butterfly) maps onto this
+// layout as: L = 16 kt + 4 e + fg, so bits 0-1 are the lane xor 16 / xor 32 levels, bits
+// 2-3 in-lane (e), bits 4-5 in-lane (kt).  Keys <= 128.
 #include "qtx_common.h"
 #include "qtx_kernels.h"
 
@@ -22,30 +31,49 @@ QTX_STAMP_SETTER(attn)
 namespace qtx {
 
 constexpr int AM_MAXK = 128;
-constexpr int AM_PS = AM_MAXK + 2;   // P row stride (floats): == 2 mod 32, conflict-free A reads
 
 // 64-byte K rows, slot swizzle of qtx_gemm.hip (conflict-free ds_read_b128 fragments)
 __device__ __forceinline__ int am_slot(int r, int c) { return c ^ (((r >> 3) & 1) << 1); }
+// staged position of key j (an involution): bits 0-1 <-> bits 2-3
+__device__ __forceinline__ int am_perm(int j) { return (j & ~15) | ((j & 3) << 2) | ((j >> 2) & 3); }
+
+// x + (x of lane ^ 16) / (lane ^ 32): one permlane swap, the pair's sum / max
+__device__ __forceinline__ float xsum16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xmax16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xmax32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 
 __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t Ks[AM_MAXK * 64];
   __shared__ __attribute__((aligned(16))) int8_t Vs[AM_MAXK * 64];
-  __shared__ float sks[AM_MAXK], svs[AM_MAXK];
-  __shared__ uint8_t mks[AM_MAXK];           // key mask when it is the same for every query
-  __shared__ float Pl[4][16 * AM_PS];
+  __shared__ __attribute__((aligned(16))) float sks[AM_MAXK];     // staged order (am_perm)
+  __shared__ __attribute__((aligned(16))) float svs[AM_MAXK];     // key order
+  __shared__ __attribute__((aligned(16))) uint8_t mks[AM_MAXK];   // per-key mask, staged order
   const int h = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
   const int Sk = a.Sk, Sq = a.Sq, hoff = h * 64;
-  const int nk4 = (Sk + 3) & ~3;            // keys rounded up to the MFMA k step
+  const int nk4 = (Sk + 3) & ~3;            // keys rounded up to the PV MFMA k step
   const int r0 = blockIdx.z * 64 + wave * 16;
   QTX_STAMP(0);
 
-  // ---- stage K, V (rows < nk4; rows >= Sk zero) and the key scales -------------------
+  // ---- stage K, V, scales, mask for all 128 key slots (slots >= Sk zero) ----------------
   const int8_t* kb = a.k + b * a.k_bs + hoff;
   const int8_t* vb = a.v + b * a.v_bs + hoff;
-  if (tid < nk4) {        // thread j stages key row j: K swizzled, V transposed (below)
-    const int j = tid, jc = min(j, Sk - 1);
+  if (tid < AM_MAXK) {    // thread j stages key j: K row at perm(j), V transposed (below)
+    const int j = tid, jc = min(j, Sk - 1), pj = am_perm(j);
     const bool ok = j < Sk;
     uint4 kv[4], vv[4];
 #pragma unroll
@@ -55,7 +83,7 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      *reinterpret_cast<uint4*>(Ks + j * 64 + 16 * am_slot(j, c)) = ok ? kv[c] : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(Ks + pj * 64 + 16 * am_slot(pj, c)) = ok ? kv[c] : make_uint4(0, 0, 0, 0);
     // Vt dword (j, f) = bytes v[j][f], v[j][16+f], v[j][32+f], v[j][48+f] (f = 0..15): the PV
     // B operand of lane (f = lane & 15) for the four 16-wide dim tiles in one ds_read_b32
     uint32_t* vt = reinterpret_cast<uint32_t*>(Vs + j * 64);
@@ -71,107 +99,116 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
       const uint32_t t23 = __builtin_amdgcn_perm(w3[q], w2[q], sel);
       vt[f] = ok ? __builtin_amdgcn_perm(t23, t01, 0x05040100u) : 0u;
     }
+    const float skj = a.sk[b * a.sk_bs + jc], svj = a.sv[b * a.sv_bs + jc];
+    sks[pj] = ok ? skj : 0.0f;
+    svs[j] = ok ? svj : 0.0f;
+    const bool row_mask = a.mask && a.m_is != 0;
+    mks[pj] = (a.mask && !row_mask && ok) ? a.mask[b * a.m_bs + j] : (uint8_t)1;
   }
   const bool row_mask = a.mask && a.m_is != 0;   // per-query mask rows (causal decoder)
-  for (int j = tid; j < nk4; j += 256) {
-    sks[j] = j < Sk ? a.sk[b * a.sk_bs + j] : 0.0f;
-    svs[j] = j < Sk ? a.sv[b * a.sv_bs + j] : 0.0f;
-    mks[j] = (a.mask && !row_mask && j < Sk) ? a.mask[b * a.m_bs + j] : (uint8_t)1;
-  }
-  // this wave's query fragment (MFMA A operand: row fr, bytes 16*fg..) and row scales
+  // this wave's query fragment (MFMA B operand: query row fr, bytes 16*fg..) and row scale
   const int qrow = min(r0 + fr, Sq - 1);
   const v4i qf = *reinterpret_cast<const v4i*>(a.q + b * a.q_bs + (long)qrow * a.q_ld + hoff + 16 * fg);
-  float sqr[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) sqr[e] = a.sq[b * a.sq_bs + min(r0 + 4 * fg + e, Sq - 1)];
+  const float sqr = a.sq[b * a.sq_bs + qrow];
   __syncthreads();
   if (r0 >= Sq) return;                    // (after the only block-wide barrier)
   QTX_STAMP(1);
 
-  // ---- scores: one i8 MFMA per 16 keys ---------------------------------------------------
-  float* P = Pl[wave];
-  for (int kt = 0; kt * 16 < Sk; ++kt) {
-    const int key = kt * 16 + fr;
-    const v4i kf = *reinterpret_cast<const v4i*>(Ks + key * 64 + 16 * am_slot(key, fg));
-    const v4i s = __builtin_amdgcn_mfma_i32_16x16x64_i8(qf, kf, v4i{0, 0, 0, 0}, 0, 0, 0);
-    const float skk = sks[key];
+  // ---- scores S^T: C[staged row 4fg + e = key 16kt + 4e + fg][query fr] ------------------
+  float x[8][4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = 4 * fg + e;          // C layout: col = key, row = 4*(lane>>4) + e
-      float sc = (((float)s[e] * sqr[e]) * skk) * 0.125f;
-      bool keep = mks[min(key, AM_MAXK - 1)] != 0;
-      if (row_mask) {
-        const int qi = min(r0 + row, Sq - 1);
-        keep = a.mask[b * a.m_bs + (long)qi * a.m_is + min(key, Sk - 1)] != 0;
+  for (int kt = 0; kt < 8; ++kt) {
+    if (16 * kt < Sk) {
+      const int krow = kt * 16 + fr;
+      const v4i kf = *reinterpret_cast<const v4i*>(Ks + krow * 64 + 16 * am_slot(krow, fg));
+      const v4i sc4 = __builtin_amdgcn_mfma_i32_16x16x64_i8(kf, qf, v4i{0, 0, 0, 0}, 0, 0, 0);
+      const int k0 = 16 * kt + 4 * fg;         // staged rows k0..k0+3
+      const float4 skv = *reinterpret_cast<const float4*>(sks + k0);
+      const uint32_t mk = *reinterpret_cast<const uint32_t*>(mks + k0);
+      const float skk[4] = {skv.x, skv.y, skv.z, skv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int key = 16 * kt + 4 * e + fg;
+        float sc = (((float)sc4[e] * sqr) * skk[e]) * 0.125f;
+        bool keep = ((mk >> (8 * e)) & 0xffu) != 0u;
+        if (row_mask) keep = a.mask[b * a.m_bs + (long)qrow * a.m_is + min(key, Sk - 1)] != 0;
+        if (!keep) sc = -1.0e9f;
+        x[kt][e] = key < Sk ? sc : -3.0e38f;
       }
-      if (!keep) sc = -1.0e9f;
-      if (key < Sk) P[row * AM_PS + key] = sc;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[kt][e] = -3.0e38f;
     }
   }
-  __builtin_amdgcn_wave_barrier();
-
   QTX_STAMP(2);
-  // ---- softmax, 4 rows per pass: the 16-lane DPP row r of the wave holds query row rb+r,
-  // lane j of it keys j + 16 i (i < 8).  Canonical order: lane-split partial of position L
-  // (L < 64) = (0 + e[L]) + e[L+64]; positions j, j+16, j+32, j+48 live in lane j, so the
-  // 64-position pairwise tree = a 16-lane tree per register, then (S0 + S1) + (S2 + S3).
-  {
-    const int sub = lane >> 4, jj = lane & 15;
-    for (int rb = 0; rb < 16; rb += 4) {
-      float* pr = P + (rb + sub) * AM_PS;
-      float x[8], e[8];
-      float m = -3.0e38f;
+
+  // ---- softmax of row fr over its 128 key slots (32 in the lane, 4 lanes) -----------------
+  float m = x[0][0];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int key = jj + 16 * i;
-        x[i] = key < Sk ? pr[key] : -3.0e38f;
-        m = fmaxf(m, x[i]);
-      }
-      m = row16_max(m);
+  for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) e[i] = (jj + 16 * i < Sk) ? qexp(x[i] - m) : 0.0f;
-      float pp[4];
+    for (int e = 0; e < 4; ++e) m = fmaxf(m, x[kt][e]);
+  m = xmax16(m);
+  m = xmax32(m);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) pp[q] = row16_sum((0.0f + e[q]) + e[q + 4]);
-      const float den = (pp[0] + pp[1]) + (pp[2] + pp[3]);
-      // e/den correctly rounded via the shared reciprocal (div_cr) unless some e is outside
-      // its range (then the true division, wave-uniform); q/127 likewise (always in range)
-      DivRange rg;
+  for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) rg.add(e[i]);
-      const bool fast = __ballot(!(rg.ok() && divisor_ok(den))) == 0ull;
-      const float rden = 1.0f / den, r127 = 1.0f / 127.0f;
-      float p[8];
-      if (fast) {
+    for (int e = 0; e < 4; ++e) x[kt][e] = (16 * kt + 4 * e + fg < Sk) ? qexp(x[kt][e] - m) : 0.0f;
+  float t[4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) p[i] = div_cr(e[i], den, rden);
-      } else {
+  for (int kt = 0; kt < 4; ++kt) {
+    float u[4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) p[i] = e[i] / den;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int key = jj + 16 * i;      // keys in [Sk, nk4) get P = 0 (padded MFMA steps)
-        const float pq = div_cr(rintf(p[i] * 127.0f), 127.0f, r127);
-        if (key < nk4) pr[key] = key < Sk ? pq : 0.0f;
-      }
-    }
+    for (int e = 0; e < 4; ++e)        // lane-split partial, then tree levels 1-2 (lanes)
+      u[e] = xsum32(xsum16((0.0f + x[kt][e]) + x[kt + 4][e]));
+    t[kt] = (u[0] + u[1]) + (u[2] + u[3]);
   }
-  __builtin_amdgcn_wave_barrier();
+  const float den = (t[0] + t[1]) + (t[2] + t[3]);
+  // e/den correctly rounded via the shared reciprocal (div_cr) unless some e is outside
+  // its range (then the true division, wave-uniform); q/127 likewise (always in range)
+  DivRange rg;
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rg.add(x[kt][e]);
+  const bool fast = __ballot(!(rg.ok() && divisor_ok(den))) == 0ull;
+  const float rden = 1.0f / den, r127 = 1.0f / 127.0f;
+  if (fast) {
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[kt][e] = div_cr(x[kt][e], den, rden);
+  } else {
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[kt][e] = x[kt][e] / den;
+  }
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {      // keys >= Sk: P = 0 (their padded PV steps add 0)
+      const float pq = div_cr(rintf(x[kt][e] * 127.0f), 127.0f, r127);
+      x[kt][e] = (16 * kt + 4 * e + fg < Sk) ? pq : 0.0f;
+    }
   QTX_STAMP(3);
-  // ---- PV on fp32 MFMA: A = P[row fr][k], B = float(v[k][d]) * s_v[k], k = 4s + fg -------
+
+  // ---- PV on fp32 MFMA: A = P[row fr][k] (the lane's x[s/4][s%4], k = 4s + fg),
+  // B = float(v[k][d]) * s_v[k] --------------------------------------------------------------
   v4f acc[4] = {v4f{0, 0, 0, 0}, v4f{0, 0, 0, 0}, v4f{0, 0, 0, 0}, v4f{0, 0, 0, 0}};
   const uint32_t* vt32 = reinterpret_cast<const uint32_t*>(Vs);
-#pragma unroll 4
-  for (int s = 0; s < nk4 / 4; ++s) {
-    const int k = 4 * s + fg;
-    const float pa = P[fr * AM_PS + k];
-    const float svk = svs[k];
-    const uint32_t vd = vt32[k * 16 + fr];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const float vb2 = (float)(int8_t)(vd >> (8 * dt)) * svk;
-      acc[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa, vb2, acc[dt], 0, 0, 0);
+  for (int s4 = 0; s4 < 32; ++s4) {
+    if (4 * s4 < nk4) {
+      const int k = 4 * s4 + fg;
+      const float pa = x[s4 >> 2][s4 & 3];
+      const float svk = svs[k];
+      const uint32_t vd = vt32[k * 16 + fr];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const float vb2 = (float)(int8_t)(vd >> (8 * dt)) * svk;
+        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa, vb2, acc[dt], 0, 0, 0);
+      }
     }
   }
 #pragma unroll

@@ -208,8 +208,8 @@ __device__ __forceinline__ unsigned abs_bits(float x) { return __float_as_uint(f
 // 2 float4 per lane, in place.  The R rows are processed step by step together so their
 // independent reduction chains overlap (ILP) instead of running one row after another.
 template <int R>
-__device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float* a, const float* b,
-                                           int lane) {
+__device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float (&ga)[2][4],
+                                           const float (&gb)[2][4]) {
   float mean[R], den[R];
 #pragma unroll
   for (int j = 0; j < R; ++j) {
@@ -241,14 +241,6 @@ __device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float* a, 
   for (int j = 0; j < R; ++j) den[j] = sqrtf(wave_sum(den[j]) / 511.0f) + 1e-6f;
   // y = (a * d) / den + b, the division correctly rounded via div_cr (one true division
   // per row for the reciprocal), true division if any value is outside div_cr's range
-  float ga[2][4], gb[2][4];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const float4 ta = *reinterpret_cast<const float4*>(a + 4 * (lane + 64 * c));
-    const float4 tb = *reinterpret_cast<const float4*>(b + 4 * (lane + 64 * c));
-    ga[c][0] = ta.x; ga[c][1] = ta.y; ga[c][2] = ta.z; ga[c][3] = ta.w;
-    gb[c][0] = tb.x; gb[c][1] = tb.y; gb[c][2] = tb.z; gb[c][3] = tb.w;
-  }
   DivRange rg;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
@@ -280,6 +272,25 @@ __device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float* a, 
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[j][c][e] = v[j][c][e] / den[j] + gb[c][e];
   }
+}
+
+// the lane's LayerNorm parameters (canonical chunks 4*lane and 256 + 4*lane), loaded once
+__device__ __forceinline__ void ln_params512(const float* a, const float* b, int lane,
+                                             float (&ga)[2][4], float (&gb)[2][4]) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float4 ta = *reinterpret_cast<const float4*>(a + 4 * (lane + 64 * c));
+    const float4 tb = *reinterpret_cast<const float4*>(b + 4 * (lane + 64 * c));
+    ga[c][0] = ta.x; ga[c][1] = ta.y; ga[c][2] = ta.z; ga[c][3] = ta.w;
+    gb[c][0] = tb.x; gb[c][1] = tb.y; gb[c][2] = tb.z; gb[c][3] = tb.w;
+  }
+}
+template <int R>
+__device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float* a, const float* b,
+                                           int lane) {
+  float ga[2][4], gb[2][4];
+  ln_params512(a, b, lane, ga, gb);
+  ln_rows512<R>(v, ga, gb);
 }
 
 // per-token quantization of R rows (2 float4 per lane each) into int8 dwords + scales

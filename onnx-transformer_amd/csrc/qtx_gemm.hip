@@ -183,25 +183,33 @@ hipError_t launch_gemm256(const GemmArgs& g, hipStream_t st) {
 }
 
 // =====================================================================================
-// k_gemm_row: 128 rows x 512 columns per workgroup (see RowGemmArgs), K step 64, four LDS
-// stages (DMA three tiles ahead; 4 x 40 KB = the whole 160 KB LDS), 8 waves as 2 (M) x
-// 4 (N), each wave 64 x 128 outputs = 4 x 8 fragments.  The epilogue works on whole
-// 512-wide row segments.
+// k_gemm_row: 128 rows x 512 columns per workgroup (see RowGemmArgs), K step 128, two LDS
+// stages of 80 KB (the whole 160 KB LDS; the DMA of tile k+1 flies during the MFMAs of
+// tile k), 8 waves as 2 (M) x 4 (N), each wave 64 x 128 outputs = 4 x 8 fragments.  The
+// epilogue works on whole 512-wide row segments.
+// K step 128 makes every DMA row a full 128-byte line (8 rows x 128 B per wave-instruction):
+// half-line pieces (16 rows x 64 B) cost the texture path twice the work per byte and held
+// the K-step-64 version of this kernel at ~16 B/clk/CU of LDS fill.
+// LDS rows are 128 B with slot swizzle c ^ ((r >> 1) & 7): conflict-free ds_read_b128
+// fragments (both 64-byte halves of the K step) for every 16-row fragment base.
 // Column order: LDS W row rho = 128 b + 16 j + f holds output column 128 b + 8 f + j, so
 // fragment j / lane column f of a wave's block is column 8 f + j: every lane holds 8
 // CONSECUTIVE columns of each of its rows (16-byte fp32 and 8-byte int8 pieces in the
 // epilogue instead of 4-byte / 1-byte ones).
 // =====================================================================================
-constexpr int R_BM = 128, R_BN = 512, R_BK = 64;
-constexpr int R_ASZ = R_BM * R_BK;                  // 8 KB
-constexpr int R_STAGE = (R_BM + R_BN) * R_BK;       // 40 KB
+constexpr int R_BM = 128, R_BN = 512, R_BK = 128;
+constexpr int R_ASZ = R_BM * R_BK;                  // 16 KB
+constexpr int R_STAGE = (R_BM + R_BN) * R_BK;       // 80 KB
 
-template <int EPI>
+__device__ __forceinline__ int r_slot(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// FULL: every row of every tile is < M (M % 128 == 0): the epilogue stores carry no row
+// guards, so no divergent branch sits between a load and its use (the compiler's counted
+// vmcnt waits would otherwise fall back to waiting for every store in flight)
+template <int EPI, bool FULL>
 __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
   __shared__ __attribute__((aligned(16))) uint8_t st0[R_STAGE];
   __shared__ __attribute__((aligned(16))) uint8_t st1[R_STAGE];
-  __shared__ __attribute__((aligned(16))) uint8_t st2[R_STAGE];
-  __shared__ __attribute__((aligned(16))) uint8_t st3[R_STAGE];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 2, wn = wave & 3;
   const int fr = lane & 15, fg = lane >> 4;
@@ -212,17 +220,22 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
   const int nk = g.K / R_BK;
   QTX_STAMP(0);
 
-  // DMA (asm: untracked by hipcc, counted by hand; see k_gemm256): wave w fills A rows
-  // 16w..16w+15 (1 instruction) and W LDS rows 64w..64w+63 (4), 5 per wave per tile
-  const int lrow = lane >> 2, lslot = lane & 3;
-  const int ra = wave * 16 + lrow;
-  const int8_t* asrc = g.A + (long)min(m0 + ra, g.M - 1) * g.lda + 16 * g_slot(ra, lslot);
-  const int8_t* wsrc[4];
+  // DMA (asm: untracked by hipcc, counted by hand; see k_gemm256): one wave-instruction
+  // fills 8 LDS rows of 128 B, lane l row l/8, slot l%8 (source chunk = slot ^ swizzle).
+  // Wave w: A rows 16w..16w+15 (2 instructions), W LDS rows 64w..64w+63 (8).
+  const int lrow = lane >> 3, lslot = lane & 7;
+  const int8_t* asrc[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int rho = wave * 64 + i * 16 + lrow;                  // LDS row
+  for (int i = 0; i < 2; ++i) {
+    const int ra = wave * 16 + i * 8 + lrow;
+    asrc[i] = g.A + (long)min(m0 + ra, g.M - 1) * g.lda + 16 * r_slot(ra, lslot);
+  }
+  const int8_t* wsrc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rho = wave * 64 + i * 8 + lrow;                   // LDS row
     const int n = (rho & ~127) + 8 * (rho & 15) + ((rho >> 4) & 7);   // its output column
-    wsrc[i] = g.W + (long)(n0 + n) * g.ldw + 16 * g_slot(rho, lslot);
+    wsrc[i] = g.W + (long)(n0 + n) * g.ldw + 16 * r_slot(rho, lslot);
   }
   auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
     const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
@@ -231,11 +244,18 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
                  "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
   };
+  // K steps in rotated order (exact int32 sums: any order gives the same accumulators):
+  // the workgroups of one XCD start at different K panels, so they do not all request the
+  // same W lines (same L2 channels) at the same time
+  const int krot = (hw >> 3) % nk;
   auto issue = [&](uint8_t* base, int kt) {
-    const int k0 = min(kt, nk - 1) * R_BK;     // past the end: harmless re-load
-    dma16(asrc + k0, base + wave * 16 * R_BK);
+    int kk = kt + krot;
+    if (kk >= nk) kk -= nk;
+    const int k0 = kk * R_BK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dma16(wsrc[i] + k0, base + R_ASZ + (wave * 64 + i * 16) * R_BK);
+    for (int i = 0; i < 2; ++i) dma16(asrc[i] + k0, base + (wave * 16 + i * 8) * R_BK);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma16(wsrc[i] + k0, base + R_ASZ + (wave * 64 + i * 8) * R_BK);
   };
 
   v4i acc[4][8];
@@ -245,59 +265,48 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
     for (int j = 0; j < 8; ++j) acc[i][j] = v4i{0, 0, 0, 0};
   auto compute = [&](const uint8_t* As) {
     const uint8_t* Bs = As + R_ASZ;
-    v4i bfr[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int r = wn * 128 + j * 16 + fr;
-      bfr[j] = *reinterpret_cast<const v4i*>(Bs + r * R_BK + 16 * g_slot(r, fg));
-    }
+    for (int h = 0; h < 2; ++h) {
+      v4i bfr[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wm * 64 + i * 16 + fr;
-      const v4i afr = *reinterpret_cast<const v4i*>(As + r * R_BK + 16 * g_slot(r, fg));
+      for (int j = 0; j < 8; ++j) {
+        const int r = wn * 128 + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const v4i*>(Bs + r * R_BK + 16 * r_slot(r, 4 * h + fg));
+      }
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, bfr[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + i * 16 + fr;
+        const v4i afr = *reinterpret_cast<const v4i*>(As + r * R_BK + 16 * r_slot(r, 4 * h + fg));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, bfr[j], acc[i][j], 0, 0, 0);
+      }
     }
   };
-  auto step = [&](uint8_t* cur, uint8_t* nxt3, int kt) {
-#ifdef QTX_STAMPS
-    if (kt == 5) QTX_STAMP(4);
-#endif
-    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // tile kt landed (kt+1, kt+2 fly)
-#ifdef QTX_STAMPS
-    if (kt == 5) QTX_STAMP(5);
-#endif
+  // step kt: tile kt landed (the only DMA in flight) and every wave is past tile kt-1, so
+  // the other stage is free for tile kt+1
+  auto step = [&](uint8_t* cur, uint8_t* nxt, int kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-#ifdef QTX_STAMPS
-    if (kt == 5) QTX_STAMP(6);
-#endif
-    issue(nxt3, kt + 3);
+    if (kt + 1 < nk) issue(nxt, kt + 1);
     compute(cur);
-#ifdef QTX_STAMPS
-    if (kt == 5) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); QTX_STAMP(7); }
-#endif
   };
   issue(st0, 0);
-  issue(st1, 1);
-  issue(st2, 2);
-  for (int kt = 0; kt < nk; kt += 4) {
-    step(st0, st3, kt);
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(st0, st1, kt);
     if (kt + 1 < nk) step(st1, st0, kt + 1);
-    if (kt + 2 < nk) step(st2, st1, kt + 2);
-    if (kt + 3 < nk) step(st3, st2, kt + 3);
   }
-  // drain the (redundant) DMAs still in flight before the epilogue reuses the LDS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  __syncthreads();                                 // all fragment reads done: LDS reusable
   QTX_STAMP(1);
 
-  // ---- y = ((float(acc) * sa[m]) * sw[n]) + b[n]; lane: rows 4*fg + e of fragment i,
-  // columns cb + j (j < 8) with cb = n0 + wn*128 + 8*fr --------------------------------
+  // ---- y = ((float(acc) * sa[m]) * sw[n]) + b[n] (relu for the FFN1 epilogues), computed
+  // once in place of the accumulators; lane: rows 4*fg + e of fragment i, columns cb + j
+  // (j < 8) with cb = n0 + wn*128 + 8*fr ------------------------------------------------
   const int cl = wn * 128 + 8 * fr;              // first of the lane's 8 columns in the tile
-  float swc[8], bc[8];
+  float y[4][8][4];
   {
+    float swc[8], bc[8];
     const float4* sp = reinterpret_cast<const float4*>(g.sw + n0 + cl);
     const float4* bp = reinterpret_cast<const float4*>(g.bias + n0 + cl);
     const float4 s0 = sp[0], s1 = sp[1], b0 = bp[0], b1 = bp[1];
@@ -305,93 +314,110 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
     swc[4] = s1.x; swc[5] = s1.y; swc[6] = s1.z; swc[7] = s1.w;
     bc[0] = b0.x; bc[1] = b0.y; bc[2] = b0.z; bc[3] = b0.w;
     bc[4] = b1.x; bc[5] = b1.y; bc[6] = b1.z; bc[7] = b1.w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float sr = g.sa[min(m0 + wm * 64 + i * 16 + 4 * fg + e, g.M - 1)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = ((float)acc[i][j][e] * sr) * swc[j] + bc[j];
+          y[i][j][e] = (EPI == RE_RELU_PMAX || EPI == RE_RELU_QUANT_PMAX) ? (v > 0.0f ? v : 0.0f) : v;
+        }
+      }
   }
-  float sr[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) sr[i][e] = g.sa[min(m0 + wm * 64 + i * 16 + 4 * fg + e, g.M - 1)];
-  // y recomputed from the int32 accumulators where needed (4 VALU ops) instead of held:
-  // 128 more live registers would spill the quantizing epilogues to scratch
-  auto yv = [&](int i, int j, int e) {
-    const float v = ((float)acc[i][j][e] * sr[i][e]) * swc[j] + bc[j];
-    return (EPI == RE_RELU_PMAX || EPI == RE_RELU_QUANT_PMAX) ? (v > 0.0f ? v : 0.0f) : v;
-  };
+  auto yv = [&](int i, int j, int e) { return y[i][j][e]; };
+  QTX_STAMP(3);
 
   if constexpr (EPI == RE_RES_LN) {
-    // x = res + y in 4 passes of 32 rows (fragment pi of both row halves): every wave
-    // stages its 16 x 128 block as fp32 rows (wm == 0 -> st0, wm == 1 -> st1), then each
-    // wave takes 4 whole rows: writes x, LayerNorm in the canonical order (ln_rows512) and
-    // per-token quant (or fp32 out).  The residual rows of pass p+1 are loaded during p.
-    float* xs0 = reinterpret_cast<float*>(st0);
-    float* xs1 = reinterpret_cast<float*>(st1);
-    float* xsw = wm == 0 ? xs0 : xs1;
-    float4 rb[2][4][2];
-    auto load_res = [&](float4 (&r)[4][2], int pi) {
+    // Two halves of 64 rows (fragments 2h, 2h+1 of both row halves): every wave stages its
+    // 32 x 128 block of y as fp32 rows in LDS (rows 0..31 of the half in st0, 32..63 in
+    // st1), then each wave takes 8 whole rows in two groups of 4: x = res + y (the residual
+    // rows loaded in the canonical lane layout, the next group's while this one works),
+    // writes x, LayerNorm in the canonical order (ln_rows512) and per-token quant (or fp32
+    // out).  Staging y without the residual frees its registers before the LN work.
+    float ga[2][4], gb[2][4];                     // LN parameters: loaded once
+    ln_params512(g.ln_a, g.ln_b, lane, ga, gb);
+    auto lds_row = [&](int r) {                   // LDS row r of the staged half (0..63)
+      return reinterpret_cast<float*>(r < 32 ? st0 : st1) + (r & 31) * R_BN;
+    };
+    // global row of LDS row r in half hh: rows wm*64 + (2hh + ii)*16 + rem
+    auto grow = [&](int hh, int r) { return m0 + (r >> 5) * 64 + (2 * hh + ((r >> 4) & 1)) * 16 + (r & 15); };
+    float4 rb[4][2];
+    auto load_res = [&](int hh, int grp) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = min(m0 + wm * 64 + pi * 16 + 4 * fg + e, g.M - 1);
-        const float4* rp = reinterpret_cast<const float4*>(g.res + (long)row * R_BN + cl);
-        r[e][0] = rp[0];
-        r[e][1] = rp[1];
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int row = min(grow(hh, 8 * wave + 4 * grp + r4), g.M - 1);
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          rb[r4][c] = *reinterpret_cast<const float4*>(g.res + (long)row * R_BN + 4 * (lane + 64 * c));
       }
     };
-    load_res(rb[0], 0);
+    load_res(0, 0);
 #pragma unroll
-    for (int pi = 0; pi < 4; ++pi) {
-      float4 (&r)[4][2] = rb[pi & 1];
-      if (pi + 1 < 4) load_res(rb[(pi + 1) & 1], pi + 1);
+    for (int hh = 0; hh < 2; ++hh) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float4* dp = reinterpret_cast<float4*>(xsw + (4 * fg + e) * R_BN + cl);
-        dp[0] = make_float4(r[e][0].x + yv(pi, 0, e), r[e][0].y + yv(pi, 1, e),
-                            r[e][0].z + yv(pi, 2, e), r[e][0].w + yv(pi, 3, e));
-        dp[1] = make_float4(r[e][1].x + yv(pi, 4, e), r[e][1].y + yv(pi, 5, e),
-                            r[e][1].z + yv(pi, 6, e), r[e][1].w + yv(pi, 7, e));
-      }
-      __syncthreads();
-      // wave w: rows 4w..4w+3 of the 32 (w < 4: st0 rows, else st1), tile row numbers
-      // pi*16 + (4w % 16) + r in its half
-      const float* xr = wave < 4 ? xs0 + (4 * wave) * R_BN : xs1 + (4 * (wave - 4)) * R_BN;
-      float v[4][2][4];
+      for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const float4 t4 = *reinterpret_cast<const float4*>(xr + r4 * R_BN + 4 * (lane + 64 * c));
-          v[r4][c][0] = t4.x; v[r4][c][1] = t4.y; v[r4][c][2] = t4.z; v[r4][c][3] = t4.w;
+        for (int e = 0; e < 4; ++e) {
+          const int i = 2 * hh + ii;
+          float4* dp = reinterpret_cast<float4*>(lds_row(wm * 32 + ii * 16 + 4 * fg + e) + cl);
+          dp[0] = make_float4(yv(i, 0, e), yv(i, 1, e), yv(i, 2, e), yv(i, 3, e));
+          dp[1] = make_float4(yv(i, 4, e), yv(i, 5, e), yv(i, 6, e), yv(i, 7, e));
         }
-      __syncthreads();                            // staging free for the next pass
-      const int rowb = m0 + (wave >> 2) * 64 + pi * 16 + 4 * (wave & 3);
+      __syncthreads();
 #pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4)
-        if (rowb + r4 < g.M)
-#pragma unroll
-          for (int c = 0; c < 2; ++c)
-            *reinterpret_cast<float4*>(g.xout + (long)(rowb + r4) * R_BN + 4 * (lane + 64 * c)) =
-                make_float4(v[r4][c][0], v[r4][c][1], v[r4][c][2], v[r4][c][3]);
-      ln_rows512<4>(v, g.ln_a, g.ln_b, lane);
-      if (g.lnq) {
-        uint32_t qd[4][2];
-        float sc[4];
-        quant_rows512<4>(v, qd, sc);
+      for (int grp = 0; grp < 2; ++grp) {
+        const bool stg = hh == 0 && grp == 0;     // diagnostic stamps (QTX_STAMPS builds)
+        if (stg) QTX_STAMP(5);
+        float v[4][2][4];
 #pragma unroll
         for (int r4 = 0; r4 < 4; ++r4)
-          if (rowb + r4 < g.M) {
-            uint32_t* qr = reinterpret_cast<uint32_t*>(g.lnq + (long)(rowb + r4) * R_BN);
-            qr[lane] = qd[r4][0];
-            qr[lane + 64] = qd[r4][1];
-            if (lane == 0) g.lns[rowb + r4] = sc[r4];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const float4 t4 = *reinterpret_cast<const float4*>(lds_row(8 * wave + 4 * grp + r4) + 4 * (lane + 64 * c));
+            v[r4][c][0] = rb[r4][c].x + t4.x; v[r4][c][1] = rb[r4][c].y + t4.y;
+            v[r4][c][2] = rb[r4][c].z + t4.z; v[r4][c][3] = rb[r4][c].w + t4.w;
           }
-      } else {
+        // the next group's residual, issued before this group's stores
+        if (grp == 0) load_res(hh, 1);
+        else if (hh == 0) load_res(1, 0);
+        if (stg) QTX_STAMP(6);
+        const int rowb = grow(hh, 8 * wave + 4 * grp);   // 4 consecutive global rows
 #pragma unroll
         for (int r4 = 0; r4 < 4; ++r4)
-          if (rowb + r4 < g.M)
+          if (FULL || rowb + r4 < g.M)
 #pragma unroll
             for (int c = 0; c < 2; ++c)
-              *reinterpret_cast<float4*>(g.lnout + (long)(rowb + r4) * R_BN + 4 * (lane + 64 * c)) =
+              *reinterpret_cast<float4*>(g.xout + (long)(rowb + r4) * R_BN + 4 * (lane + 64 * c)) =
                   make_float4(v[r4][c][0], v[r4][c][1], v[r4][c][2], v[r4][c][3]);
+        if (stg) QTX_STAMP(7);
+        ln_rows512<4>(v, ga, gb);
+        if (stg) QTX_STAMP(8);
+        if (g.lnq) {
+          uint32_t qd[4][2];
+          float sc[4];
+          quant_rows512<4>(v, qd, sc);
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4)
+            if (FULL || rowb + r4 < g.M) {
+              uint32_t* qr = reinterpret_cast<uint32_t*>(g.lnq + (long)(rowb + r4) * R_BN);
+              qr[lane] = qd[r4][0];
+              qr[lane + 64] = qd[r4][1];
+              if (lane == 0) g.lns[rowb + r4] = sc[r4];
+            }
+        } else {
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4)
+            if (FULL || rowb + r4 < g.M)
+#pragma unroll
+              for (int c = 0; c < 2; ++c)
+                *reinterpret_cast<float4*>(g.lnout + (long)(rowb + r4) * R_BN + 4 * (lane + 64 * c)) =
+                    make_float4(v[r4][c][0], v[r4][c][1], v[r4][c][2], v[r4][c][3]);
+        }
+        if (stg) QTX_STAMP(9);
       }
+      __syncthreads();                            // staging free for the next half
     }
     QTX_STAMP(2);
     return;
@@ -434,6 +460,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
         rmax[i][e] = fmaxf(fmaxf(red[rl], red[R_BM + rl]), fmaxf(red[2 * R_BM + rl], red[3 * R_BM + rl]));
       }
   }
+  QTX_STAMP(4);
   if constexpr (EPI == RE_RELU_PMAX) {
     if (wn == 0 && fr == 0)
 #pragma unroll
@@ -441,7 +468,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int row = m0 + wm * 64 + i * 16 + 4 * fg + e;
-          if (row < g.M) g.pmax_out[(long)t * g.M + row] = rmax[i][e];
+          if (FULL || row < g.M) g.pmax_out[(long)t * g.M + row] = rmax[i][e];
         }
     QTX_STAMP(2);
     return;
@@ -471,7 +498,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
           int qv[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) qv[j] = (int)rintf(quot(yv(i, j, e), sc[i][e], inv[i][e]));
-          if (row < g.M)                  // the lane's 8 consecutive columns: one 8-byte store
+          if (FULL || row < g.M)          // the lane's 8 consecutive columns: one 8-byte store
             *reinterpret_cast<uint2*>(ob + (long)row * g.ldo8 + cl) =
                 make_uint2(pack4_i8(qv[0], qv[1], qv[2], qv[3]), pack4_i8(qv[4], qv[5], qv[6], qv[7]));
         }
@@ -488,7 +515,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int row = m0 + wm * 64 + i * 16 + 4 * fg + e;
-            if (row < g.M) osp[row] = sc[i][e];
+            if (FULL || row < g.M) osp[row] = sc[i][e];
           }
     }
     QTX_STAMP(2);
@@ -501,13 +528,18 @@ hipError_t launch_gemm_row(const RowGemmArgs& g, hipStream_t st) {
     return hipErrorInvalidValue;
   if (g.epi == RE_RES_LN && g.N != R_BN) return hipErrorInvalidValue;
   const dim3 grid((g.N / R_BN) * ((g.M + R_BM - 1) / R_BM)), block(512);
+  const bool full = g.M % R_BM == 0;
+#define QTX_ROW_LAUNCH(E)                                                           \
+  (full ? (k_gemm_row<E, true><<<grid, block, 0, st>>>(g), 0)                       \
+        : (k_gemm_row<E, false><<<grid, block, 0, st>>>(g), 0))
   switch (g.epi) {
-    case RE_QUANT: k_gemm_row<RE_QUANT><<<grid, block, 0, st>>>(g); break;
-    case RE_RES_LN: k_gemm_row<RE_RES_LN><<<grid, block, 0, st>>>(g); break;
-    case RE_RELU_PMAX: k_gemm_row<RE_RELU_PMAX><<<grid, block, 0, st>>>(g); break;
-    case RE_RELU_QUANT_PMAX: k_gemm_row<RE_RELU_QUANT_PMAX><<<grid, block, 0, st>>>(g); break;
+    case RE_QUANT: QTX_ROW_LAUNCH(RE_QUANT); break;
+    case RE_RES_LN: QTX_ROW_LAUNCH(RE_RES_LN); break;
+    case RE_RELU_PMAX: QTX_ROW_LAUNCH(RE_RELU_PMAX); break;
+    case RE_RELU_QUANT_PMAX: QTX_ROW_LAUNCH(RE_RELU_QUANT_PMAX); break;
     default: return hipErrorInvalidValue;
   }
+#undef QTX_ROW_LAUNCH
   return hipGetLastError();
 }
 

@@ -131,7 +131,10 @@ def test_linear_asymmetric_identity(torch, M):
 
 
 @pytest.mark.parametrize("B,Sq,Sk,masked", [(2, 20, 20, True), (3, 1, 37, False),
-                                            (2, 128, 128, True), (1, 7, 300, True)])
+                                            (2, 128, 128, True), (1, 7, 300, True),
+                                            (3, 128, 128, "key"), (2, 72, 72, "key"),
+                                            (2, 65, 100, "key"), (2, 16, 64, "key"),
+                                            (1, 130, 5, "key")])
 def test_attention(torch, B, Sq, Sk, masked):
     rng = np.random.default_rng(Sq * 7 + Sk)
     H = 8
@@ -140,13 +143,20 @@ def test_attention(torch, B, Sq, Sk, masked):
     v = rng.integers(-127, 128, (B, Sk, 512)).astype(np.int8)
     sq, sk, sv = (rng.uniform(0.002, 0.03, (B, n)).astype(f32) for n in (Sq, Sk, Sk))
     mask = np.ones((B, Sq, Sk), np.uint8)
-    if masked:
+    m_bs, m_is, mdev = Sq * Sk, Sk, mask
+    if masked == "key":               # encoder form: one key mask per sentence (m_is = 0)
+        km = np.ones((B, Sk), np.uint8)
+        km[0, Sk - Sk // 3:] = 0
+        km[-1, 1::7] = 0
+        mask[:] = km[:, None, :]
+        m_bs, m_is, mdev = Sk, 0, km
+    elif masked:
         mask[-1, :, Sk // 2:] = 0
         mask[0] = np.tril(np.ones((Sq, Sk), np.uint8), k=Sk - Sq)
     ctx = torch.empty((B, Sq, 512), dtype=torch.float32, device="cuda")
     call("qtx_attention_i8", P(dev(torch, q)), P(dev(torch, sq)), P(dev(torch, k)),
-         P(dev(torch, sk)), P(dev(torch, v)), P(dev(torch, sv)), P(dev(torch, mask)),
-         Sq * Sk, Sk, B, H, Sq, Sk, P(ctx), S0)
+         P(dev(torch, sk)), P(dev(torch, v)), P(dev(torch, sv)), P(dev(torch, mdev)),
+         m_bs, m_is, B, H, Sq, Sk, P(ctx), S0)
     co, _ = O.attention(q, sq, k, sk, v, sv, mask, H)
     np.testing.assert_array_equal(ctx.cpu().numpy(), co)
 

@@ -43,6 +43,8 @@ for name, N, K, a, kw in cases:
     for k, v in base.items():
         setattr(args, k, v.data_ptr() if hasattr(v, "data_ptr") else v)
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if stamps is not None:
+        stamps.zero_()
     for _ in range(3):
         assert L.qtx_linear_rows(C.byref(args), st) == 0, L.qtx_last_error()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -57,9 +59,14 @@ for name, N, K, a, kw in cases:
     ops = 2 * M * N * K
     extra = ""
     if stamps is not None:
-        s = stamps[:1024, :8].cpu().numpy().astype(np.float64)
-        d = np.median(np.diff(s[:, :3], axis=1), 0).astype(int).tolist()
-        tl = np.median(np.diff(s[:, 4:8], axis=1), 0).astype(int).tolist()
-        extra = f"  phases(main loop, epilogue) {d} cyc; tile 5 (vmcnt, barrier, compute) {tl}"
+        nblk = (N // 512) * (M // 128)
+        s = stamps[:nblk, :16].cpu().numpy().astype(np.float64)
+        if kw["epi"] == 1:
+            d = np.median(np.diff(s[:, [0, 1, 3, 2]], axis=1), 0).astype(int).tolist()
+            gq = np.median(np.diff(s[:, 5:10], axis=1), 0).astype(int).tolist()
+            extra = f"  cyc (main loop, y, res+LN+quant) {d}; group 0 (v, xout, LN, quant+st) {gq}"
+        else:
+            d = np.median(np.diff(s[:, [0, 1, 3, 4, 2]], axis=1), 0).astype(int).tolist()
+            extra = f"  cyc (main loop, y, row max, quant/store) {d}"
     print(f"{name:12s} {t * 1e6:7.1f} us  {100 * ops / t / PEAK:5.1f} % of int8 peak{extra}")
 print(f"layer (5 launches) {tot * 1e6:.1f} us")
