@@ -138,6 +138,16 @@ int32_t qtx_attention_i8(const int8_t* q, const float* sq, const int8_t* k, cons
                          int64_t m_is, int32_t B, int32_t H, int32_t Sq, int32_t Sk,
                          float* ctx, void* stream);
 
+/* Encoder self-attention with the context quantized per token for the O-projection
+ * (attention.py:23-67 + quant_linear.py:30-43, replacing the MatMul_{8L+3,8L+4} pair of the
+ * encoder graph and the following QuantizeLinear): q/k/v int8 [B,S,512] (8 heads) +
+ * per-token scales [B,S], key mask uint8 [B,S] (NULL = keep all) -> ctx8 int8 [B,S,512] +
+ * sctx [B,S].  S <= 128.  One workgroup per sentence. */
+int32_t qtx_attention_i8_quant(const int8_t* q, const float* sq, const int8_t* k,
+                               const float* sk, const int8_t* v, const float* sv,
+                               const uint8_t* key_mask, int32_t B, int32_t S, int8_t* ctx8,
+                               float* sctx, void* stream);
+
 /* ---- fused decode-step kernels (the KV-cached greedy step is built from these) ---- */
 
 /* Row-complete int8 GEMM (8-bit weights, N % 512 == 0, K % 64 == 0) whose epilogue sees

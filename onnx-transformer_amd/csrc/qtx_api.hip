@@ -502,8 +502,15 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
     RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st));
     AttnArgs a = attn_args(s, B, S, S, S);
     a.mask = mask; a.m_bs = S; a.m_is = 0;
-    HIPCHK(launch_attention(a, st));
-    RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+    a.c_ld = D;
+    const hipError_t ea = getenv("QTX_NO_ATTN_ENCQ") ? hipErrorNotSupported
+                                                     : launch_attention_encq(a, s.a8, s.sa, st);
+    if (ea == hipErrorNotSupported) {    // other shapes: fp32 context + quantization kernel
+      HIPCHK(launch_attention(a, st));
+      RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+    } else {
+      HIPCHK(ea);
+    }
     RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st));
     RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st));
     if (l + 1 < NL)
@@ -889,8 +896,15 @@ int32_t qtx_decoder_forward(const qtx_model* m, const float* y, const float* mem
     RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st));
     AttnArgs a = attn_args(s, B, T, T, T);
     a.mask = tgt_mask; a.m_bs = tm_bs; a.m_is = T;
-    HIPCHK(launch_attention(a, st));
-    RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+    a.c_ld = D;
+    const hipError_t ea = getenv("QTX_NO_ATTN_ENCQ") ? hipErrorNotSupported
+                                                     : launch_attention_encq(a, s.a8, s.sa, st);
+    if (ea == hipErrorNotSupported) {    // other shapes: fp32 context + quantization kernel
+      HIPCHK(launch_attention(a, st));
+      RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+    } else {
+      HIPCHK(ea);
+    }
     RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st));
     RC(row_quant(L.cq, s.a8, s.sa, M, s.q8, s.sq, st));
     a = attn_args(s, B, T, S, S);
@@ -1178,6 +1192,24 @@ int32_t qtx_decode_attention(int32_t kv_new, const float* y, int64_t ldy, int8_t
 int32_t qtx_pack_int4(const int8_t* q, int32_t N, int32_t K, uint8_t* packed, void* stream) {
   if (!q || !packed || K % 2) return fail(QTX_E_INVALID, "bad argument");
   HIPCHK(launch_pack_int4(q, N, K, packed, (hipStream_t)stream));
+  return QTX_OK;
+}
+
+int32_t qtx_attention_i8_quant(const int8_t* q, const float* sq, const int8_t* k,
+                               const float* sk, const int8_t* v, const float* sv,
+                               const uint8_t* key_mask, int32_t B, int32_t S, int8_t* ctx8,
+                               float* sctx, void* stream) {
+  if (!q || !sq || !k || !sk || !v || !sv || !ctx8 || !sctx) return fail(QTX_E_INVALID, "null argument");
+  if (B <= 0 || S <= 0 || S > 128) return fail(QTX_E_UNSUPPORTED, "S=%d (1..128)", S);
+  const long D = 512;
+  AttnArgs a{};
+  a.q = q; a.q_bs = S * D; a.q_ld = D; a.sq = sq; a.sq_bs = S;
+  a.k = k; a.k_bs = S * D; a.k_ld = D; a.sk = sk; a.sk_bs = S;
+  a.v = v; a.v_bs = S * D; a.v_ld = D; a.sv = sv; a.sv_bs = S;
+  a.mask = key_mask; a.m_bs = S; a.m_is = 0;
+  a.c_bs = S * D; a.c_ld = D;
+  a.B = B; a.H = 8; a.Sq = S; a.Sk = S;
+  HIPCHK(launch_attention_encq(a, ctx8, sctx, (hipStream_t)stream, true));
   return QTX_OK;
 }
 

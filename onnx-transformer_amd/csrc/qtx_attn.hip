@@ -229,4 +229,237 @@ hipError_t launch_attention_mfma(const AttnArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+
+// =====================================================================================
+// k_attn_encq: encoder self-attention of ONE sentence, all heads, with the context
+// quantized per token in the epilogue (attention.py:23-67 + the O-projection's input
+// quantizer, quant_linear.py:30-43): no fp32 context round trip through HBM and no
+// separate quantization kernel.
+//
+// Workgroup = sentence b, 8 waves; wave w owns query rows 16w..16w+15 and ALL 8 heads,
+// so each lane ends with 4 whole-row segments (rows 4fg+e, 32 dims each) and the row
+// absmax needs only the 16 lanes of its DPP row.  K and V of every head (2 x 64 KB) are
+// staged once by LDS-DMA (global_load_lds_dwordx4, 2 key rows of 512 B per wave
+// instruction): K rows in the staged key order am_perm with chunk swizzle
+// slot = chunk ^ (row & 15) (conflict-free ds_read_b128 fragments for every head), V rows
+// in key order with slot = chunk ^ 4 (row & 1) (conflict-free ds_read_b32 operands).
+// Per head: S^T = K Q^T on i8 MFMA (Q fragments straight from HBM, one head ahead),
+// softmax + P-quant in registers (the canonical trees of k_attn_mfma), PV on f32 MFMA
+// with the output column n of dim tile dt = head dim 4n + dt, so one ds_read_b32 of a
+// row-major V row feeds the four dim tiles of a k step.
+// =====================================================================================
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for_(F& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_<I + 1, N>(f);
+  }
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) { static_for_<0, N>(f); }
+
+__device__ __forceinline__ void dma16_lds(const void* gsrc, const void* lds_dst) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+}
+
+__global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, float* sctx) {
+  __shared__ __attribute__((aligned(16))) uint8_t Ks[AM_MAXK * 512];
+  __shared__ __attribute__((aligned(16))) uint8_t Vs[AM_MAXK * 512];
+  __shared__ __attribute__((aligned(16))) float sks[AM_MAXK];     // s_k / 8 (0 if masked), staged order
+  __shared__ __attribute__((aligned(16))) float kadd[AM_MAXK];    // 0 kept, -1e9 masked, -3e38 absent
+  __shared__ __attribute__((aligned(16))) float svs[AM_MAXK];     // s_v, key order
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int Sk = a.Sk, Sq = a.Sq;
+  const int r0 = wave * 16;
+  QTX_STAMP(0);
+
+  // ---- stage K and V of all heads: wave w moves LDS rows 16w..16w+15 of each ----------
+  {
+    const int rp = lane >> 5, slot = lane & 31;
+    const int8_t* kb = a.k + b * a.k_bs;
+    const int8_t* vb = a.v + b * a.v_bs;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int p = wave * 16 + 2 * i + rp;                 // LDS row of this lane
+      const int kk = min(am_perm(p), Sk - 1), kv = min(p, Sk - 1);
+      dma16_lds(kb + (long)kk * a.k_ld + 16 * (slot ^ (p & 15)), Ks + (wave * 16 + 2 * i) * 512);
+      dma16_lds(vb + (long)kv * a.v_ld + 16 * (slot ^ (4 * (p & 1))), Vs + (wave * 16 + 2 * i) * 512);
+    }
+  }
+  if (tid < AM_MAXK) {
+    // score of key j = ((float(acc) * s_q) * (s_k / 8 or 0)) + kadd: the exact form of
+    // ((acc * s_q) * s_k) / 8 then masked_fill(-1e9) (kept: x + 0 == x; masked:
+    // x * 0 - 1e9 == -1e9; / 8 is exact and commutes with rounding for these normal
+    // magnitudes); keys >= Sk get -3e38, so their e and P come out exactly 0 with no
+    // per-element test
+    const int j = tid, jc = min(j, Sk - 1), pj = am_perm(j);
+    const bool ok = j < Sk;
+    const float skj = a.sk[b * a.sk_bs + jc], svj = a.sv[b * a.sv_bs + jc];
+    const bool keep = ok && (!a.mask || a.mask[b * a.m_bs + jc] != 0);
+    sks[pj] = keep ? skj * 0.125f : 0.0f;
+    kadd[pj] = !ok ? -3.0e38f : (keep ? 0.0f : -1.0e9f);
+    svs[j] = ok ? svj : 0.0f;
+  }
+  const int qrow = min(r0 + fr, Sq - 1);
+  const int8_t* qbase = a.q + b * a.q_bs + (long)qrow * a.q_ld + 16 * fg;
+  v4i qf = *reinterpret_cast<const v4i*>(qbase);
+  const float sqr = a.sq[b * a.sq_bs + qrow];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (r0 >= Sq) return;                    // (after the only block-wide barrier)
+  QTX_STAMP(1);
+
+  v4f ctx[8][4];
+#pragma unroll
+  for (int h = 0; h < 8; ++h)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) ctx[h][dt] = v4f{0, 0, 0, 0};
+
+  // the head loop is unrolled by instantiation (ctx[h] must be register-resident: a
+  // run-time head index would put the 128 accumulators in scratch)
+  static_for<8>([&](auto hc) {
+    constexpr int h = decltype(hc)::value;
+    __builtin_amdgcn_sched_barrier(0);
+    if (h == 0) QTX_STAMP(4);
+    const v4i qcur = qf;
+    if (h < 7) qf = *reinterpret_cast<const v4i*>(qbase + 64 * (h + 1));   // next head
+    // ---- scores S^T: C[staged row 4fg + e = key 16kt + 4e + fg][query fr] --------------
+    float x[8][4];
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      if (16 * kt < Sk) {
+        const int krow = kt * 16 + fr;
+        const v4i kf = *reinterpret_cast<const v4i*>(Ks + krow * 512 + 16 * ((4 * h + fg) ^ fr));
+        const v4i sc4 = __builtin_amdgcn_mfma_i32_16x16x64_i8(kf, qcur, v4i{0, 0, 0, 0}, 0, 0, 0);
+        const int k0 = 16 * kt + 4 * fg;         // staged rows k0..k0+3
+        const float4 skv = *reinterpret_cast<const float4*>(sks + k0);
+        const float4 kav = *reinterpret_cast<const float4*>(kadd + k0);
+        const float skk[4] = {skv.x, skv.y, skv.z, skv.w};
+        const float kak[4] = {kav.x, kav.y, kav.z, kav.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[kt][e] = ((float)sc4[e] * sqr) * skk[e] + kak[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[kt][e] = -3.0e38f;
+      }
+    }
+    if (h == 0) QTX_STAMP(5);
+    // ---- softmax of row fr over its key slots (32 in the lane, 4 lanes), the canonical
+    // trees of k_attn_mfma.  Absent keys: qexp(-3e38 - m) == 0 exactly.
+    float m = x[0][0];
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m = fmaxf(m, x[kt][e]);
+    m = xmax16(m);
+    m = xmax32(m);
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[kt][e] = qexp(x[kt][e] - m);
+    float t[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      float u[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) u[e] = xsum32(xsum16((0.0f + x[kt][e]) + x[kt + 4][e]));
+      t[kt] = (u[0] + u[1]) + (u[2] + u[3]);
+    }
+    const float den = (t[0] + t[1]) + (t[2] + t[3]);
+    // P = rint((e / den) * 127) / 127 with both divisions by div_cr, unguarded: den is in
+    // [1, 128] (the row max contributes qexp(0) == 1), so e / den is correctly rounded for
+    // every e >= 2^-60, and e < 2^-60 (or 0) gives P == 0 through either quotient
+    const float rden = 1.0f / den, r127 = 1.0f / 127.0f;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        x[kt][e] = div_cr(rintf(div_cr(x[kt][e], den, rden) * 127.0f), 127.0f, r127);
+    __builtin_amdgcn_sched_barrier(0);
+    if (h == 0) QTX_STAMP(6);
+    // ---- PV: A = P[row fr][k = 4 s4 + fg], B[k][n] = float(v[k][64h + 4n + dt]) * s_v[k] --
+    const uint8_t* vrow = Vs + fg * 512 + 16 * ((4 * h + (fr >> 2)) ^ (4 * (fg & 1))) + 4 * (fr & 3);
+    // in chunks of 32 keys with no branch inside (the V operand reads of a chunk are
+    // issued ahead of its MFMAs); padded keys of a chunk have P == 0 and s_v == 0, so
+    // their steps add +0 to a nonzero-or-+0 accumulator: exact
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (32 * c < Sk) {
+#pragma unroll
+        for (int s4 = 8 * c; s4 < 8 * c + 8; ++s4) {
+          const float pa = x[s4 >> 2][s4 & 3];
+          const float svk = svs[4 * s4 + fg];
+          const uint32_t vd = *reinterpret_cast<const uint32_t*>(vrow + s4 * 2048);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const float vb2 = (float)(int8_t)(vd >> (8 * dt)) * svk;
+            ctx[h][dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa, vb2, ctx[h][dt], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (h == 0) QTX_STAMP(7);
+  });
+  QTX_STAMP(2);
+
+  // ---- per-token quantization of the context rows 4fg + e (dims 64h + 4fr + dt):
+  // rint(y / s) with y / s by div_cr — exact for a whole row when its absmax < 2^37 (as
+  // the GEMM epilogues, qtx_gemm.hip); otherwise the true division (wave-uniform) -------
+  float sc[4], inv[4];
+  bool big = false;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float am = 0.0f;
+#pragma unroll
+    for (int h = 0; h < 8; ++h)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) am = fmaxf(am, fabsf(ctx[h][dt][e]));
+    am = row16_max(am);
+    sc[e] = quant_scale(am, 127.0f);
+    inv[e] = 1.0f / sc[e];
+    big |= !(am < 0x1p37f);
+  }
+  auto store_rows = [&](auto quot) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = r0 + 4 * fg + e;
+      if (row < Sq) {
+        uint32_t* orow = reinterpret_cast<uint32_t*>(ctx8 + ((long)b * Sq + row) * a.c_ld) + fr;
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+          int qv[4];
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) qv[dt] = (int)rintf(quot(ctx[h][dt][e], sc[e], inv[e]));
+          orow[16 * h] = pack4_i8(qv[0], qv[1], qv[2], qv[3]);
+        }
+        if (fr == 0) sctx[(long)b * Sq + row] = sc[e];
+      }
+    }
+  };
+  if (__builtin_expect(__ballot(big) != 0ull, 0))
+    store_rows([](float y, float s, float) { return y / s; });
+  else
+    store_rows([](float y, float s, float r) { return div_cr(y, s, r); });
+  QTX_STAMP(3);
+}
+
+// Encoder self-attention with the per-token-quantized context (int8 [B,S,512] with row
+// stride a.c_ld, scales [B*S]); H == 8, Sq == Sk <= 128, per-key mask (m_is == 0).
+hipError_t launch_attention_encq(const AttnArgs& a, int8_t* ctx8, float* sctx, hipStream_t st,
+                                 bool force_encq) {
+  if (a.sk_dev || a.qpos_dev || a.H != 8 || a.Sk <= 0 || a.Sk > AM_MAXK || a.Sq != a.Sk ||
+      (a.mask && a.m_is != 0) || (a.k_ld % 16) || (a.v_ld % 16) || (a.c_ld % 4))
+    return hipErrorNotSupported;
+  if (a.B < 128 && !force_encq) return hipErrorNotSupported;   // one workgroup per sentence:
+  // below ~128 sentences the per-(head, query block) kernel spreads over more CUs
+  k_attn_encq<<<dim3(a.B), dim3(512), 0, st>>>(a, ctx8, sctx);
+  return hipGetLastError();
+}
+
 }  // namespace qtx

@@ -145,6 +145,11 @@ hipError_t launch_step_inc(int* step, hipStream_t st);
 hipError_t launch_nop(hipStream_t st);
 hipError_t launch_gemm256(const GemmArgs& g, hipStream_t st);
 hipError_t launch_attention_mfma(const AttnArgs& a, hipStream_t st);
+// encoder self-attention, all heads of a sentence per workgroup, context quantized per
+// token -> ctx8 (row stride a.c_ld) + sctx; hipErrorNotSupported unless H == 8,
+// Sq == Sk <= 128 and the mask is per key (m_is == 0), and (unless forced) B >= 128
+hipError_t launch_attention_encq(const AttnArgs& a, int8_t* ctx8, float* sctx, hipStream_t st,
+                                 bool force_encq = false);
 hipError_t launch_fill_col(int64_t* ids, long bs, int B, int64_t val, hipStream_t st);
 
 }  // namespace qtx

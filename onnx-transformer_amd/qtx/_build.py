@@ -43,19 +43,37 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(f) <= t for f in _inputs())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile the library if any source is newer; returns its path."""
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = False, extra=()) -> str:
+    """Compile the library if any source is newer; returns its path.  Each source is
+    compiled to a relocatable gfx950 object in parallel (-fgpu-rdc is not needed: no
+    cross-file device symbols), then linked into one shared library."""
+    from concurrent.futures import ThreadPoolExecutor
+    out = LIB if not extra else LIB.replace(".so", "_diag.so")
+    if not force and not extra and up_to_date():
         return LIB
-    tmp = LIB + ".tmp"
-    cmd = [hipcc(), *FLAGS, "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]
-    if verbose:
-        print(" ".join(cmd))
+    objdir = os.path.join(HERE, "build_obj")
+    os.makedirs(objdir, exist_ok=True)
+    cflags = [f for f in FLAGS if f != "-shared"] + list(extra)
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ("_x" if extra else "") + ".o")
+        cmd = [hipcc(), *cflags, "-c", "-o", obj, os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src} ({r.returncode}):\n{r.stderr[-4000:]}")
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = out + ".tmp"
+    cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-4000:]}")
-    os.replace(tmp, LIB)
-    return LIB
+        raise RuntimeError(f"hipcc link failed ({r.returncode}):\n{r.stderr[-4000:]}")
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

@@ -161,6 +161,29 @@ def test_attention(torch, B, Sq, Sk, masked):
     np.testing.assert_array_equal(ctx.cpu().numpy(), co)
 
 
+@pytest.mark.parametrize("B,S,keymask", [(3, 128, True), (2, 72, True), (2, 5, False),
+                                          (1, 1, False), (4, 100, True), (2, 128, False)])
+def test_attention_quant(torch, B, S, keymask):
+    """Encoder attention with the per-token-quantized context (k_attn_encq) == oracle
+    attention followed by the O-projection input quantizer, bit for bit."""
+    rng = np.random.default_rng(S * 11 + B)
+    q, k, v = (rng.integers(-127, 128, (B, S, 512)).astype(np.int8) for _ in range(3))
+    sq, sk, sv = (rng.uniform(0.002, 0.03, (B, S)).astype(f32) for _ in range(3))
+    km = np.ones((B, S), np.uint8)
+    if keymask:
+        km[0, S - S // 3:] = 0
+        km[-1, 1::7] = 0
+    ctx8 = torch.empty((B, S, 512), dtype=torch.int8, device="cuda")
+    sctx = torch.empty((B, S), dtype=torch.float32, device="cuda")
+    call("qtx_attention_i8_quant", P(dev(torch, q)), P(dev(torch, sq)), P(dev(torch, k)),
+         P(dev(torch, sk)), P(dev(torch, v)), P(dev(torch, sv)),
+         P(dev(torch, km)) if keymask else S0, B, S, P(ctx8), P(sctx), S0)
+    co, _ = O.attention(q, sq, k, sk, v, sv, km[:, None, :], 8)
+    qc, sc = O.quant_rows(co)
+    np.testing.assert_array_equal(sctx.cpu().numpy(), sc)
+    np.testing.assert_array_equal(ctx8.cpu().numpy(), qc)
+
+
 def test_embed(torch, gpu_model, golden_ops, oracle_model):
     # The PE table is computed at load time by torch's CPU sin/cos (as the reference
     # does), whose last ulp depends on the host CPU; compare with the oracle on the same
