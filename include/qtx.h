@@ -100,6 +100,56 @@ int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t*
                           int32_t B, int32_t S, int32_t max_len, int64_t start, int64_t* ids,
                           void* ws, size_t ws_bytes, void* stream);
 
+/* ---- fault injection (the reference's campaigns: inject_utils/layers.py:48-84,
+ * onnx_optimized_inference.py:59-204, parallelized_inject_onnx_transformer.py:536-720) ----
+ * One fault per run, at one QuantLinear MatMul of one module.  Targets use the reference's
+ * ONNX MatMul numbering: encoder layer L MatMul_{8L+i}, i = QTX_LIN_Q/K/V/O/
+ * FFN1/FFN2; decoder layer L MatMul_{12+12L+i} (self Q/K/V/O, cross Q/O, FFN) and the
+ * memory K/V projections MatMul_{2L}, MatMul_{2L+1} (QTX_LIN_CK / QTX_LIN_CV).
+ * Kinds (rows index the module's flattened [B*S] or [B*T] tokens; cross K/V: memory tokens):
+ *   INPUT     bit `bit` of the int8 input q[row, col] flipped (every output column)
+ *   WEIGHT    bit `bit` of the int8 weight q[row = out channel, col] flipped (every row)
+ *   INPUT16   as INPUT, the output perturbation kept on columns win_start .. +win_len (<= 16)
+ *   WEIGHT16  as WEIGHT, the perturbation kept on rows win_start .. +win_len (<= 16)
+ *   OUTPUT    the MatMul output (before bias) at (row, col) replaced by `value`
+ *             (RANDOM: a random float; RANDOM_BITFLIP: a bit-flipped golden value)
+ * Requires 8-bit weights. */
+typedef enum {
+  QTX_FAULT_NONE = 0, QTX_FAULT_INPUT = 1, QTX_FAULT_WEIGHT = 2, QTX_FAULT_INPUT16 = 3,
+  QTX_FAULT_WEIGHT16 = 4, QTX_FAULT_OUTPUT = 5
+} qtx_fault_kind;
+typedef enum {
+  QTX_LIN_Q = 0, QTX_LIN_K = 1, QTX_LIN_V = 2, QTX_LIN_O = 5, QTX_LIN_FFN1 = 6,
+  QTX_LIN_FFN2 = 7, QTX_LIN_CQ = 8, QTX_LIN_CK = 9, QTX_LIN_CV = 10, QTX_LIN_CO = 11
+} qtx_linear_id;
+typedef struct {
+  int32_t kind;      /* qtx_fault_kind */
+  int32_t module;    /* 0 encoder, 1 decoder */
+  int32_t layer;
+  int32_t linear;    /* qtx_linear_id */
+  int64_t row, col;  /* see the kinds above */
+  int64_t win_start;
+  int32_t win_len;
+  int32_t bit;       /* 0..7 */
+  float value;       /* OUTPUT */
+  int32_t reserved;
+} qtx_fault;
+
+/* qtx_encoder_forward / qtx_decoder_forward / qtx_greedy_decode with one fault (host
+ * pointer; NULL or kind NONE = golden run).  The greedy decode takes encoder faults. */
+int32_t qtx_encoder_forward_fault(const qtx_model* m, const float* x, const uint8_t* src_mask,
+                                  int32_t B, int32_t S, float* out, void* ws, size_t ws_bytes,
+                                  const qtx_fault* fault, void* stream);
+int32_t qtx_decoder_forward_fault(const qtx_model* m, const float* y, const float* memory,
+                                  const uint8_t* src_mask, const uint8_t* tgt_mask,
+                                  int32_t tgt_mask_batched, int32_t B, int32_t T, int32_t S,
+                                  float* out, void* ws, size_t ws_bytes,
+                                  const qtx_fault* fault, void* stream);
+int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
+                                const uint8_t* src_mask, int32_t B, int32_t S, int32_t max_len,
+                                int64_t start, int64_t* ids, void* ws, size_t ws_bytes,
+                                const qtx_fault* fault, void* stream);
+
 /* Embeddings + positional encoding: which = 0 (src) / 1 (tgt); ids int64 [B,T] ->
  * out [B,T,d], positions pos0 .. pos0+T-1. */
 int32_t qtx_embed(const qtx_model* m, int32_t which, const int64_t* ids, int32_t B, int32_t T,

@@ -403,16 +403,19 @@ RowGemmArgs rowgemm(const QLin& L, const int8_t* a8, const float* sa, int M, int
 }
 // out = per-token quantized (a8 . W^T) per 512-wide tile into out8 + t*M*512, os + t*M
 int row_quant(const QLin& L, const int8_t* a8, const float* sa, int M, int8_t* out8,
-              float* os, hipStream_t st) {
+              float* os, hipStream_t st, const FaultArgs& fa = FaultArgs{}) {
   RowGemmArgs g = rowgemm(L, a8, sa, M, RE_QUANT);
+  g.fault = fa;
   g.out8 = out8; g.ldo8 = 512; g.o8_ts = (long)M * 512; g.os = os; g.os_ts = M;
   HIPCHK(launch_gemm_row(g, st));
   return QTX_OK;
 }
 // x += a8 . W^T, then LayerNorm(x) (ln) quantized into (lnq, lns) or fp32 into lnout
 int row_res_ln(const QLin& L, const int8_t* a8, const float* sa, int M, float* x,
-               const float* const* ln, int8_t* lnq, float* lns, float* lnout, hipStream_t st) {
+               const float* const* ln, int8_t* lnq, float* lns, float* lnout, hipStream_t st,
+               const FaultArgs& fa = FaultArgs{}) {
   RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RES_LN);
+  g.fault = fa;
   g.res = x; g.xout = x; g.ln_a = ln[0]; g.ln_b = ln[1];
   g.lnq = lnq; g.lns = lns; g.lnout = lnout;
   HIPCHK(launch_gemm_row(g, st));
@@ -421,8 +424,10 @@ int row_res_ln(const QLin& L, const int8_t* a8, const float* sa, int M, float* x
 // FFN1: relu(a8 . W1^T) quantized per token over all d_ff columns, two passes (row
 // maxima, then recompute + quantize: cheaper than the fp32 hidden's round trip)
 int row_ffn1(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa, int M,
-             Scratch& s, hipStream_t st) {
+             Scratch& s, hipStream_t st,
+             const FaultArgs& fa = FaultArgs{}) {
   RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RELU_PMAX);
+  g.fault = fa;
   g.pmax_out = s.pmax;
   HIPCHK(launch_gemm_row(g, st));
   g.epi = RE_RELU_QUANT_PMAX;
@@ -479,8 +484,82 @@ int ffn_block(const qtx_config& c, const QLin& w1, const QLin& w2, const float* 
   return QTX_OK;
 }
 
+
+// ---- fault injection (qtx_fault, include/qtx.h) -------------------------------------
+// The GEMM that computes a given reference MatMul, and that linear's column offset in it.
+enum GemmId { G_QKV, G_O, G_FFN1, G_FFN2, G_CQ, G_CKV, G_CO };
+FaultArgs fault_for(const qtx_fault* f, int module, int layer, GemmId gid, int M,
+                    const qtx_config& c) {
+  FaultArgs fa{};
+  if (!f || f->kind == QTX_FAULT_NONE || f->module != module || f->layer != layer) return fa;
+  const int lin = f->linear;
+  long off = 0, nlin = c.d_model;
+  switch (gid) {
+    case G_QKV: if (lin < QTX_LIN_Q || lin > QTX_LIN_V) return fa; off = (long)lin * c.d_model; break;
+    case G_CKV: if (lin != QTX_LIN_CK && lin != QTX_LIN_CV) return fa;
+                off = (long)(lin - QTX_LIN_CK) * c.d_model; break;
+    case G_O: if (lin != QTX_LIN_O) return fa; break;
+    case G_FFN1: if (lin != QTX_LIN_FFN1) return fa; nlin = c.d_ff; break;
+    case G_FFN2: if (lin != QTX_LIN_FFN2) return fa; break;
+    case G_CQ: if (lin != QTX_LIN_CQ) return fa; break;
+    case G_CO: if (lin != QTX_LIN_CO) return fa; break;
+  }
+  fa.bit = f->bit;
+  switch (f->kind) {
+    case QTX_FAULT_INPUT: case QTX_FAULT_INPUT16:
+      fa.kind = FK_INPUT; fa.row = f->row; fa.col = f->col;
+      fa.lo = off + (f->kind == QTX_FAULT_INPUT16 ? f->win_start : 0);
+      fa.hi = f->kind == QTX_FAULT_INPUT16 ? fa.lo + f->win_len : off + nlin;
+      break;
+    case QTX_FAULT_WEIGHT: case QTX_FAULT_WEIGHT16:
+      fa.kind = FK_WEIGHT; fa.row = off + f->row; fa.col = f->col;
+      fa.lo = f->kind == QTX_FAULT_WEIGHT16 ? f->win_start : 0;
+      fa.hi = f->kind == QTX_FAULT_WEIGHT16 ? fa.lo + f->win_len : M;
+      break;
+    case QTX_FAULT_OUTPUT:
+      fa.kind = FK_OUTPUT; fa.row = f->row; fa.col = off + f->col; fa.value = f->value;
+      break;
+  }
+  return fa;
+}
+
+// Validates a fault against the shapes of its target MatMul (M token rows of the module,
+// Ms memory rows for the decoder's cross K/V); returns QTX_OK or an error code.
+int check_fault(const qtx_model* m, const qtx_fault* f, int module, long M, long Ms) {
+  if (!f || f->kind == QTX_FAULT_NONE) return QTX_OK;
+  const qtx_config& c = m->cfg;
+  if (!row_path(c)) return fail(QTX_E_UNSUPPORTED, "fault injection needs 8-bit weights");
+  if (f->kind < 0 || f->kind > QTX_FAULT_OUTPUT) return fail(QTX_E_INVALID, "fault kind %d", f->kind);
+  if (f->module != module) return fail(QTX_E_INVALID, "fault module %d", f->module);
+  if (f->layer < 0 || f->layer >= c.n_layers) return fail(QTX_E_INVALID, "fault layer %d", f->layer);
+  const int lin = f->linear;
+  const bool enc_ok = lin == QTX_LIN_Q || lin == QTX_LIN_K || lin == QTX_LIN_V || lin == QTX_LIN_O ||
+                      lin == QTX_LIN_FFN1 || lin == QTX_LIN_FFN2;
+  const bool dec_ok = enc_ok || (lin >= QTX_LIN_CQ && lin <= QTX_LIN_CO);
+  if (!(module == 0 ? enc_ok : dec_ok)) return fail(QTX_E_INVALID, "fault linear %d", lin);
+  const long rows = (lin == QTX_LIN_CK || lin == QTX_LIN_CV) ? Ms : M;
+  const long K = lin == QTX_LIN_FFN2 ? c.d_ff : c.d_model;
+  const long N = lin == QTX_LIN_FFN1 ? c.d_ff : c.d_model;
+  const bool in_kind = f->kind == QTX_FAULT_INPUT || f->kind == QTX_FAULT_INPUT16;
+  const bool w_kind = f->kind == QTX_FAULT_WEIGHT || f->kind == QTX_FAULT_WEIGHT16;
+  if ((in_kind || w_kind) && (f->bit < 0 || f->bit > 7)) return fail(QTX_E_INVALID, "fault bit %d", f->bit);
+  if (in_kind && (f->row < 0 || f->row >= rows || f->col < 0 || f->col >= K))
+    return fail(QTX_E_INVALID, "input fault index (%ld, %ld) outside [%ld, %ld]", (long)f->row, (long)f->col, rows, K);
+  if (w_kind && (f->row < 0 || f->row >= N || f->col < 0 || f->col >= K))
+    return fail(QTX_E_INVALID, "weight fault index (%ld, %ld) outside [%ld, %ld]", (long)f->row, (long)f->col, N, K);
+  if (f->kind == QTX_FAULT_OUTPUT && (f->row < 0 || f->row >= rows || f->col < 0 || f->col >= N))
+    return fail(QTX_E_INVALID, "output fault index (%ld, %ld) outside [%ld, %ld]", (long)f->row, (long)f->col, rows, N);
+  if (f->kind == QTX_FAULT_INPUT16 &&
+      (f->win_len < 1 || f->win_len > 16 || f->win_start < 0 || f->win_start + f->win_len > N))
+    return fail(QTX_E_INVALID, "INPUT16 window");
+  if (f->kind == QTX_FAULT_WEIGHT16 &&
+      (f->win_len < 1 || f->win_len > 16 || f->win_start < 0 || f->win_start + f->win_len > rows))
+    return fail(QTX_E_INVALID, "WEIGHT16 window");
+  return QTX_OK;
+}
+
 int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, int S,
-                float* out, Scratch& s, hipStream_t st) {
+                float* out, Scratch& s, hipStream_t st, const qtx_fault* f = nullptr) {
   const qtx_config& c = m->cfg;
   const int D = c.d_model, M = B * S;
   if (x != s.x) HIPCHK(hipMemcpyAsync(s.x, x, (size_t)M * D * 4, hipMemcpyDeviceToDevice, st));
@@ -499,7 +578,8 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
   RC(ln_quant(s.x, M, m->enc[0].ln[0], D, s.a8, s.sa, st));
   for (int l = 0; l < NL; ++l) {
     const EncLayer& L = m->enc[l];
-    RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st));
+    auto fa = [&](GemmId gid) { return fault_for(f, 0, l, gid, M, c); };
+    RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st, fa(G_QKV)));
     AttnArgs a = attn_args(s, B, S, S, S);
     a.mask = mask; a.m_bs = S; a.m_is = 0;
     a.c_ld = D;
@@ -511,12 +591,12 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
     } else {
       HIPCHK(ea);
     }
-    RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st));
-    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st));
+    RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st, fa(G_O)));
+    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1)));
     if (l + 1 < NL)
-      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc[l + 1].ln[0], s.a8, s.sa, nullptr, st));
+      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc[l + 1].ln[0], s.a8, s.sa, nullptr, st, fa(G_FFN2)));
     else
-      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc_norm, nullptr, nullptr, out, st));
+      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc_norm, nullptr, nullptr, out, st, fa(G_FFN2)));
   }
   return QTX_OK;
 }
@@ -552,13 +632,15 @@ CrossKV carve_cross(Arena& ar, const qtx_config& c, long Ms) {
 }
 
 // memory -> per-layer cross K/V (get_quantized_model.py:160-168: K/V outputs quantized)
-int cross_kv(const qtx_model* m, const float* memory, int Ms, CrossKV& x, hipStream_t st) {
+int cross_kv(const qtx_model* m, const float* memory, int Ms, CrossKV& x, hipStream_t st,
+             const qtx_fault* f = nullptr) {
   const qtx_config& c = m->cfg;
   const int D = c.d_model;
   RC(quant(memory, D, Ms, D, x.am8, x.sam, st));
   for (int l = 0; l < c.n_layers; ++l) {
     if (row_path(c)) {     // K and V tiles quantized in the GEMM epilogue
-      RC(row_quant(m->dec[l].ckv, x.am8, x.sam, Ms, x.k8[l], x.sk[l], st));
+      RC(row_quant(m->dec[l].ckv, x.am8, x.sam, Ms, x.k8[l], x.sk[l], st,
+                   fault_for(f, 1, l, G_CKV, Ms, c)));
       continue;
     }
     RC(linear(c, m->dec[l].ckv, x.am8, x.sam, Ms, 0, nullptr, x.y, 2 * D, st));
@@ -846,27 +928,36 @@ size_t qtx_greedy_workspace_size(const qtx_model* m, int32_t B, int32_t S, int32
   return align_up(ar.used);
 }
 
-int32_t qtx_encoder_forward(const qtx_model* m, const float* x, const uint8_t* src_mask,
-                            int32_t B, int32_t S, float* out, void* ws, size_t ws_bytes,
-                            void* stream) {
+int32_t qtx_encoder_forward_fault(const qtx_model* m, const float* x, const uint8_t* src_mask,
+                                  int32_t B, int32_t S, float* out, void* ws, size_t ws_bytes,
+                                  const qtx_fault* f, void* stream) {
   if (!m || !x || !src_mask || !out || !ws) return fail(QTX_E_INVALID, "null argument");
   if (B <= 0 || S <= 0 || S > 512) return fail(QTX_E_INVALID, "bad shape B=%d S=%d", B, S);
   if (ws_bytes < enc_ws(m->cfg, B, S)) return fail(QTX_E_WORKSPACE, "workspace too small");
+  RC(check_fault(m, f, 0, (long)B * S, 0));
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
   Scratch s = carve_scratch(ar, m->cfg, (long)B * S);
-  return encoder_run(m, x, src_mask, B, S, out, s, (hipStream_t)stream);
+  return encoder_run(m, x, src_mask, B, S, out, s, (hipStream_t)stream, f);
 }
 
-int32_t qtx_decoder_forward(const qtx_model* m, const float* y, const float* memory,
-                            const uint8_t* src_mask, const uint8_t* tgt_mask,
-                            int32_t tgt_mask_batched, int32_t B, int32_t T, int32_t S,
-                            float* out, void* ws, size_t ws_bytes, void* stream) {
+int32_t qtx_encoder_forward(const qtx_model* m, const float* x, const uint8_t* src_mask,
+                            int32_t B, int32_t S, float* out, void* ws, size_t ws_bytes,
+                            void* stream) {
+  return qtx_encoder_forward_fault(m, x, src_mask, B, S, out, ws, ws_bytes, nullptr, stream);
+}
+
+int32_t qtx_decoder_forward_fault(const qtx_model* m, const float* y, const float* memory,
+                                  const uint8_t* src_mask, const uint8_t* tgt_mask,
+                                  int32_t tgt_mask_batched, int32_t B, int32_t T, int32_t S,
+                                  float* out, void* ws, size_t ws_bytes, const qtx_fault* f,
+                                  void* stream) {
   if (!m || !y || !memory || !src_mask || !tgt_mask || !out || !ws)
     return fail(QTX_E_INVALID, "null argument");
   if (B <= 0 || T <= 0 || S <= 0 || T > 512 || S > 512)
     return fail(QTX_E_INVALID, "bad shape B=%d T=%d S=%d", B, T, S);
   if (ws_bytes < dec_ws(m->cfg, B, T, S)) return fail(QTX_E_WORKSPACE, "workspace too small");
+  RC(check_fault(m, f, 1, (long)B * T, (long)B * S));
   hipStream_t st = (hipStream_t)stream;
   const qtx_config& c = m->cfg;
   const int D = c.d_model, M = B * T;
@@ -874,7 +965,7 @@ int32_t qtx_decoder_forward(const qtx_model* m, const float* y, const float* mem
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
   Scratch s = carve_scratch(ar, c, M);
   CrossKV x = carve_cross(ar, c, (long)B * S);
-  RC(cross_kv(m, memory, B * S, x, st));
+  RC(cross_kv(m, memory, B * S, x, st, f));
   HIPCHK(hipMemcpyAsync(s.x, y, (size_t)M * D * 4, hipMemcpyDeviceToDevice, st));
   const long tm_bs = tgt_mask_batched ? (long)T * T : 0;
   if (!row_path(c)) {
@@ -893,7 +984,8 @@ int32_t qtx_decoder_forward(const qtx_model* m, const float* y, const float* mem
   RC(ln_quant(s.x, M, m->dec[0].ln[0], D, s.a8, s.sa, st));
   for (int l = 0; l < NL; ++l) {
     const DecLayer& L = m->dec[l];
-    RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st));
+    auto fa = [&](GemmId gid) { return fault_for(f, 1, l, gid, M, c); };
+    RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st, fa(G_QKV)));
     AttnArgs a = attn_args(s, B, T, T, T);
     a.mask = tgt_mask; a.m_bs = tm_bs; a.m_is = T;
     a.c_ld = D;
@@ -905,21 +997,29 @@ int32_t qtx_decoder_forward(const qtx_model* m, const float* y, const float* mem
     } else {
       HIPCHK(ea);
     }
-    RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st));
-    RC(row_quant(L.cq, s.a8, s.sa, M, s.q8, s.sq, st));
+    RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st, fa(G_O)));
+    RC(row_quant(L.cq, s.a8, s.sa, M, s.q8, s.sq, st, fa(G_CQ)));
     a = attn_args(s, B, T, S, S);
     a.k = x.k8[l]; a.sk = x.sk[l]; a.v = x.v8[l]; a.sv = x.sv[l];
     a.mask = src_mask; a.m_bs = S; a.m_is = 0;
     HIPCHK(launch_attention(a, st));
     RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
-    RC(row_res_ln(L.co, s.a8, s.sa, M, s.x, L.ln[2], s.a8, s.sa, nullptr, st));
-    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st));
+    RC(row_res_ln(L.co, s.a8, s.sa, M, s.x, L.ln[2], s.a8, s.sa, nullptr, st, fa(G_CO)));
+    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1)));
     if (l + 1 < NL)
-      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->dec[l + 1].ln[0], s.a8, s.sa, nullptr, st));
+      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->dec[l + 1].ln[0], s.a8, s.sa, nullptr, st, fa(G_FFN2)));
     else
-      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->dec_norm, nullptr, nullptr, out, st));
+      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->dec_norm, nullptr, nullptr, out, st, fa(G_FFN2)));
   }
   return QTX_OK;
+}
+
+int32_t qtx_decoder_forward(const qtx_model* m, const float* y, const float* memory,
+                            const uint8_t* src_mask, const uint8_t* tgt_mask,
+                            int32_t tgt_mask_batched, int32_t B, int32_t T, int32_t S,
+                            float* out, void* ws, size_t ws_bytes, void* stream) {
+  return qtx_decoder_forward_fault(m, y, memory, src_mask, tgt_mask, tgt_mask_batched, B, T, S,
+                                   out, ws, ws_bytes, nullptr, stream);
 }
 
 int32_t qtx_embed(const qtx_model* m, int32_t which, const int64_t* ids, int32_t B, int32_t T,
@@ -947,9 +1047,10 @@ int32_t qtx_generator(const qtx_model* m, const float* x, int32_t M, float* logp
   return QTX_OK;
 }
 
-int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t* src_mask,
-                          int32_t B, int32_t S, int32_t max_len, int64_t start, int64_t* ids,
-                          void* ws, size_t ws_bytes, void* stream) {
+int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
+                                const uint8_t* src_mask, int32_t B, int32_t S, int32_t max_len,
+                                int64_t start, int64_t* ids, void* ws, size_t ws_bytes,
+                                const qtx_fault* f, void* stream) {
   if (!m || !src || !src_mask || !ids || !ws) return fail(QTX_E_INVALID, "null argument");
   const qtx_config& c = m->cfg;
   if (B <= 0 || S <= 0 || S > 512 || max_len < 1 || max_len > 512 || max_len > c.max_len ||
@@ -957,6 +1058,10 @@ int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t*
     return fail(QTX_E_INVALID, "bad shape B=%d S=%d max_len=%d", B, S, max_len);
   if (ws_bytes < qtx_greedy_workspace_size(m, B, S, max_len))
     return fail(QTX_E_WORKSPACE, "workspace too small");
+  if (f && f->kind != QTX_FAULT_NONE && f->module != 0)
+    return fail(QTX_E_UNSUPPORTED, "greedy decode takes encoder faults (decoder faults: "
+                                   "qtx_decoder_forward_fault on the step's prefix)");
+  RC(check_fault(m, f, 0, (long)B * S, 0));
   hipStream_t st = (hipStream_t)stream;
   const int D = c.d_model;
   Arena ar;
@@ -966,7 +1071,7 @@ int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t*
   // encoder: memory = encode(src_embed(src), src_mask)
   HIPCHK(launch_embed(src, S, B, S, nullptr, 0, m->src_lut, c.src_vocab, m->pe, c.max_len,
                       g.enc.x, (long)S * D, st));
-  RC(encoder_run(m, g.enc.x, src_mask, B, S, g.memory, g.enc, st));
+  RC(encoder_run(m, g.enc.x, src_mask, B, S, g.memory, g.enc, st, f));
   RC(cross_kv(m, g.memory, B * S, g.cross, st));
 
   // ids[:, 0] = start ; step[0] = position 0, step[1] = arrival counter
@@ -1080,6 +1185,13 @@ int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t*
       HIPCHK(hipStreamWaitEvent(st, mm->ev_out[i], 0));
     }
   return QTX_OK;
+}
+
+int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t* src_mask,
+                          int32_t B, int32_t S, int32_t max_len, int64_t start, int64_t* ids,
+                          void* ws, size_t ws_bytes, void* stream) {
+  return qtx_greedy_decode_fault(m, src, src_mask, B, S, max_len, start, ids, ws, ws_bytes,
+                                 nullptr, stream);
 }
 
 // ---- per-op entry points ---------------------------------------------------------------

@@ -299,6 +299,30 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
   }
   __syncthreads();                                 // all fragment reads done: LDS reusable
   QTX_STAMP(1);
+  if (g.fault.kind == FK_INPUT || g.fault.kind == FK_WEIGHT) {
+    // exact integer correction of the accumulators for one bit-flipped int8 operand
+    // (the perturbation the reference propagates through the MatMul, inject_utils/layers.py)
+    const FaultArgs& f = g.fault;
+    const bool inp = f.kind == FK_INPUT;
+    const int8_t orig = inp ? g.A[f.row * g.lda + f.col] : g.W[f.row * g.ldw + f.col];
+    const int delta = (int)(int8_t)(orig ^ (1 << f.bit)) - (int)orig;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long row = m0 + wm * 64 + i * 16 + 4 * fg + e;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const long col = n0 + wn * 128 + 8 * fr + j;
+          if (row < g.M) {
+            if (inp && row == f.row && col >= f.lo && col < f.hi)
+              acc[i][j][e] += delta * (int)g.W[col * g.ldw + f.col];
+            if (!inp && col == f.row && row >= f.lo && row < f.hi)
+              acc[i][j][e] += delta * (int)g.A[row * g.lda + f.col];
+          }
+        }
+      }
+  }
 
   // ---- y = ((float(acc) * sa[m]) * sw[n]) + b[n] (relu for the FFN1 epilogues), computed
   // once in place of the accumulators; lane: rows 4*fg + e of fragment i, columns cb + j
@@ -325,6 +349,20 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
           y[i][j][e] = (EPI == RE_RELU_PMAX || EPI == RE_RELU_QUANT_PMAX) ? (v > 0.0f ? v : 0.0f) : v;
         }
       }
+    if (g.fault.kind == FK_OUTPUT) {   // RANDOM fault models: one MatMul output value replaced
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const long row = m0 + wm * 64 + i * 16 + 4 * fg + e;
+            if (row == g.fault.row && n0 + cl + j == g.fault.col) {
+              const float v = g.fault.value + bc[j];
+              y[i][j][e] = (EPI == RE_RELU_PMAX || EPI == RE_RELU_QUANT_PMAX) ? (v > 0.0f ? v : 0.0f) : v;
+            }
+          }
+    }
   }
   auto yv = [&](int i, int j, int e) { return y[i][j][e]; };
   QTX_STAMP(3);

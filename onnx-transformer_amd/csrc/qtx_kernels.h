@@ -102,6 +102,18 @@ struct AttnArgs {
 //   RE_RELU_QUANT_PMAX  relu(y) quantized per token with the max over pmax_in [pmax_n][M]
 //                       -> out8 [M,N] (ld ldo8) + os [M]                 (FFN1, 2nd pass)
 enum RowEpi { RE_QUANT = 0, RE_RES_LN = 1, RE_RELU_PMAX = 2, RE_RELU_QUANT_PMAX = 3 };
+// Fault injected into one row-GEMM launch (the reference's fault models, qtx.h qtx_fault),
+// in GEMM-local coordinates:
+//   FK_INPUT   A[row, col] bit-flipped: acc[row, n] += (flip(a) - a) * W[n, col], n in [lo, hi)
+//   FK_WEIGHT  W[row, col] bit-flipped: acc[m, row] += A[m, col] * (flip(w) - w), m in [lo, hi)
+//   FK_OUTPUT  the MatMul output (before bias) at (row, col) replaced by value
+enum { FK_NONE = 0, FK_INPUT = 1, FK_WEIGHT = 2, FK_OUTPUT = 3 };
+struct FaultArgs {
+  int kind, bit;
+  long row, col, lo, hi;
+  float value;
+};
+
 struct RowGemmArgs {
   const int8_t* A; long lda; const float* sa;
   const int8_t* W; long ldw; const float* sw; const float* bias;
@@ -110,6 +122,7 @@ struct RowGemmArgs {
   const float* res; float* xout; const float* ln_a; const float* ln_b;
   int8_t* lnq; float* lns; float* lnout;
   float* pmax_out; const float* pmax_in; int pmax_n;
+  FaultArgs fault;                          // kind FK_NONE: no fault (the product path)
 };
 hipError_t launch_gemm_row(const RowGemmArgs& a, hipStream_t st);
 

@@ -41,6 +41,15 @@ class RowGemm(C.Structure):
                 ("lnq", P), ("lns", P), ("lnout", P),
                 ("pmax_out", P), ("pmax_in", P), ("pmax_n", I32)]
 
+class Fault(C.Structure):
+    """struct qtx_fault (include/qtx.h)."""
+    _fields_ = [("kind", I32), ("module", I32), ("layer", I32), ("linear", I32),
+                ("row", I64), ("col", I64), ("win_start", I64), ("win_len", I32),
+                ("bit", I32), ("value", F32), ("reserved", I32)]
+
+
+FP = C.POINTER(Fault)
+
 # name -> (restype, argtypes); must match include/qtx.h
 SIGNATURES = {
     "qtx_last_error": (C.c_char_p, []),
@@ -55,6 +64,9 @@ SIGNATURES = {
     "qtx_encoder_forward": (I32, [P, P, P, I32, I32, P, P, SZ, P]),
     "qtx_decoder_forward": (I32, [P, P, P, P, P, I32, I32, I32, I32, P, P, SZ, P]),
     "qtx_greedy_decode": (I32, [P, P, P, I32, I32, I32, I64, P, P, SZ, P]),
+    "qtx_encoder_forward_fault": (I32, [P, P, P, I32, I32, P, P, SZ, FP, P]),
+    "qtx_decoder_forward_fault": (I32, [P, P, P, P, P, I32, I32, I32, I32, P, P, SZ, FP, P]),
+    "qtx_greedy_decode_fault": (I32, [P, P, P, I32, I32, I32, I64, P, P, SZ, FP, P]),
     "qtx_embed": (I32, [P, I32, P, I32, I32, I32, P, P]),
     "qtx_generator": (I32, [P, P, I32, P, P, P, SZ, P]),
     "qtx_row_quant": (I32, [P, I32, I32, F32, P, P, P]),

@@ -83,18 +83,23 @@ class QtxModel:
         return self._ws
 
     # ---- model-level entry points (device tensors in, device tensors out) -------------
-    def encode(self, x, src_mask_u8):
-        """x [B,S,512] f32, src_mask_u8 [B,S] uint8 -> memory [B,S,512] f32."""
+    def encode(self, x, src_mask_u8, fault=None):
+        """x [B,S,512] f32, src_mask_u8 [B,S] uint8 -> memory [B,S,512] f32.
+        fault: an optional qtx.fault.Fault (one injected fault, module "Encoder")."""
         torch = _torch()
         B, S, _ = x.shape
         out = torch.empty_like(x)
         nb = _lib.lib().qtx_encoder_workspace_size(self.handle, B, S)
         ws = self.workspace(nb)
-        _lib.call("qtx_encoder_forward", self.handle, _ptr(x), _ptr(src_mask_u8), B, S,
-                  _ptr(out), _ptr(ws), ws.numel(), _stream())
+        if fault is None:
+            _lib.call("qtx_encoder_forward", self.handle, _ptr(x), _ptr(src_mask_u8), B, S,
+                      _ptr(out), _ptr(ws), ws.numel(), _stream())
+        else:
+            _lib.call("qtx_encoder_forward_fault", self.handle, _ptr(x), _ptr(src_mask_u8), B,
+                      S, _ptr(out), _ptr(ws), ws.numel(), C.byref(fault.to_c()), _stream())
         return out
 
-    def decode(self, y, memory, src_mask_u8, tgt_mask_u8):
+    def decode(self, y, memory, src_mask_u8, tgt_mask_u8, fault=None):
         """y [B,T,512], memory [B,S,512], src_mask [B,S] u8, tgt_mask [T,T] or [B,T,T] u8."""
         torch = _torch()
         B, T, _ = y.shape
@@ -103,21 +108,32 @@ class QtxModel:
         nb = _lib.lib().qtx_decoder_workspace_size(self.handle, B, T, S)
         ws = self.workspace(nb)
         batched = 1 if tgt_mask_u8.dim() == 3 and tgt_mask_u8.shape[0] == B and B > 1 else 0
-        _lib.call("qtx_decoder_forward", self.handle, _ptr(y), _ptr(memory), _ptr(src_mask_u8),
-                  _ptr(tgt_mask_u8), batched, B, T, S, _ptr(out), _ptr(ws), ws.numel(),
-                  _stream())
+        if fault is None:
+            _lib.call("qtx_decoder_forward", self.handle, _ptr(y), _ptr(memory),
+                      _ptr(src_mask_u8), _ptr(tgt_mask_u8), batched, B, T, S, _ptr(out),
+                      _ptr(ws), ws.numel(), _stream())
+        else:
+            _lib.call("qtx_decoder_forward_fault", self.handle, _ptr(y), _ptr(memory),
+                      _ptr(src_mask_u8), _ptr(tgt_mask_u8), batched, B, T, S, _ptr(out),
+                      _ptr(ws), ws.numel(), C.byref(fault.to_c()), _stream())
         return out
 
-    def greedy(self, src, src_mask_u8, max_len: int = 72, start: int = 0, out=None):
-        """src int64 [B,S], src_mask [B,S] u8 -> ids int64 [B,max_len] (device)."""
+    def greedy(self, src, src_mask_u8, max_len: int = 72, start: int = 0, out=None, fault=None):
+        """src int64 [B,S], src_mask [B,S] u8 -> ids int64 [B,max_len] (device).
+        fault: an optional encoder qtx.fault.Fault."""
         torch = _torch()
         B, S = src.shape
         ids = out if out is not None else torch.empty((B, max_len), dtype=torch.int64,
                                                       device=self.device)
         nb = _lib.lib().qtx_greedy_workspace_size(self.handle, B, S, max_len)
         ws = self.workspace(nb)
-        _lib.call("qtx_greedy_decode", self.handle, _ptr(src), _ptr(src_mask_u8), B, S,
-                  max_len, int(start), _ptr(ids), _ptr(ws), ws.numel(), _stream())
+        if fault is None:
+            _lib.call("qtx_greedy_decode", self.handle, _ptr(src), _ptr(src_mask_u8), B, S,
+                      max_len, int(start), _ptr(ids), _ptr(ws), ws.numel(), _stream())
+        else:
+            _lib.call("qtx_greedy_decode_fault", self.handle, _ptr(src), _ptr(src_mask_u8), B,
+                      S, max_len, int(start), _ptr(ids), _ptr(ws), ws.numel(),
+                      C.byref(fault.to_c()), _stream())
         return ids
 
     def embed(self, ids, which: str = "src", pos0: int = 0):

@@ -60,7 +60,7 @@ def _shape(a):
     return tuple(a.shape)
 
 
-def run_encoder(model: QtxModel, feeds: dict):
+def run_encoder(model: QtxModel, feeds: dict, fault=None):
     """global_in f32 [B,S,512], global_in_1 bool [B,1,S] -> global_out f32 [B,S,512]."""
     import torch
     _check(feeds, ENCODER_FEEDS)
@@ -72,10 +72,10 @@ def run_encoder(model: QtxModel, feeds: dict):
         raise ValueError(f"global_in_1: expected [B,1,S]=[{B},1,{S}], got {_shape(m)}")
     xd = _as_torch(x, model.device, torch.float32)
     md = to_u8_mask(m, model.device).reshape(B, S)
-    return model.encode(xd, md)
+    return model.encode(xd, md, fault=fault)
 
 
-def run_decoder(model: QtxModel, feeds: dict):
+def run_decoder(model: QtxModel, feeds: dict, fault=None):
     """global_in [B,T,512], global_in_1 memory [B,S,512], global_in_2 [B,1,S],
     global_in_3 int64 [1,T,T] (or [B,T,T]) -> global_out [B,T,512]."""
     import torch
@@ -97,7 +97,7 @@ def run_decoder(model: QtxModel, feeds: dict):
     smd = to_u8_mask(sm, model.device).reshape(B, S)
     tmd = to_u8_mask(tm, model.device)
     tmd = tmd.reshape(T, T) if int(np.prod(ts)) == T * T else tmd.reshape(B, T, T)
-    return model.decode(yd, md, smd, tmd)
+    return model.decode(yd, md, smd, tmd, fault=fault)
 
 
 class InferenceSession:
@@ -128,17 +128,42 @@ class InferenceSession:
 
 
 def run_module(module, input_values, module_filepath=None, module_weight_dict=None,
-               module_graph=None, inject_parameters=None, model: QtxModel | None = None):
-    """onnx_optimized_inference.py:297-304 contract: returns (output_tensors, weight_dict)."""
-    if inject_parameters:
-        raise NotImplementedError("fault injection hooks are not implemented yet (SURVEY §8f)")
+               module_graph=None, inject_parameters=None, model: QtxModel | None = None,
+               rng=None):
+    """onnx_optimized_inference.py:297-304 contract: returns (output_tensors, weight_dict).
+
+    inject_parameters: the reference's dict (inject_type INPUT/WEIGHT/INPUT16/WEIGHT16/
+    RANDOM/RANDOM_BITFLIP, faulty_operation_name "MatMul_<n>", targetted_module,
+    faulty_bit_position; parallelized_inject_onnx_transformer.py:837-858), or a
+    qtx.fault.Fault.  One fault is injected into this run; the drawn fault is stored in
+    weight_dict["qtx_fault"] (the reference records its choice in the experiment log)."""
+    from . import fault as F
     model = model or _default_model
     if model is None:
         raise ValueError("no QtxModel: pass model= or call qtx.set_default_model()")
     weight_dict = {} if module_weight_dict is None else module_weight_dict
     for k, v in input_values.items():
         weight_dict[k] = v
-    fn = run_encoder if _module_kind(module) == "encoder" else run_decoder
-    out = fn(model, input_values).cpu().numpy()
+    kind = _module_kind(module)
+    fn = run_encoder if kind == "encoder" else run_decoder
+    flt = None
+    if inject_parameters:
+        if isinstance(inject_parameters, F.Fault):
+            flt = inject_parameters
+        else:
+            x = input_values["global_in"]
+            rows = int(np.prod(_shape(x)[:2]))
+            mod, _, lin = F.matmul_target(inject_parameters["faulty_operation_name"],
+                                          inject_parameters.get("targetted_module", kind))
+            if lin in ("CK", "CV"):
+                rows = int(np.prod(_shape(input_values["global_in_1"])[:2]))
+            golden = None
+            if inject_parameters["inject_type"] == "RANDOM_BITFLIP":
+                raise ValueError("RANDOM_BITFLIP needs the golden MatMul output: draw the "
+                                 "fault with qtx.fault.random_fault(golden_output=...)")
+            flt = F.from_inject_parameters(dict(inject_parameters, targetted_module=kind), rows,
+                                           rng, model.cfg.n_layers, golden)
+        weight_dict["qtx_fault"] = flt
+    out = fn(model, input_values, flt).cpu().numpy()
     weight_dict["global_out"] = out
     return {"global_out": out}, weight_dict

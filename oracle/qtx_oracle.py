@@ -179,11 +179,36 @@ class QLinear:
         self.q, self.s = quant_weight(w, n_bits)
         self.b = np.asarray(b, f32)
 
-    def __call__(self, x, relu=False, quantize_output=False):
-        """W8A8Linear.forward (quant_linear.py:111-119) on an fp32 input x [..., K]."""
+    def __call__(self, x, relu=False, quantize_output=False, fault=None):
+        """W8A8Linear.forward (quant_linear.py:111-119) on an fp32 input x [..., K].
+
+        fault (optional, fault-injection runs): dict with kind INPUT/INPUT16/WEIGHT/
+        WEIGHT16/OUTPUT and row, col, bit, lo, hi, value in this linear's coordinates
+        (rows = flattened tokens) — the reference's fault models
+        (inject_utils/layers.py:48-84, onnx_optimized_inference.py:59-204): a bit-flipped
+        int8 operand propagated through the MatMul (restricted to a window for *16), or
+        one MatMul output (before bias) replaced by ``value``."""
         shp = x.shape
         qx, sx = quant_rows(x.reshape(-1, shp[-1]))
-        y = linear_epilogue(int_gemm(qx, self.q), sx, self.s, self.b, relu=relu)
+        acc = int_gemm(qx, self.q)
+        if fault is not None and fault["kind"] != "OUTPUT":
+            flip = lambda v: np.int8(np.uint8(np.int8(v).view(np.uint8) ^ (1 << fault["bit"])).view(np.int8))
+            r, c, lo, hi = fault["row"], fault["col"], fault["lo"], fault["hi"]
+            if fault["kind"].startswith("INPUT"):
+                qx2 = qx.copy()
+                qx2[r, c] = flip(qx2[r, c])
+                acc2 = int_gemm(qx2, self.q)
+                acc[r, lo:hi] = acc2[r, lo:hi]
+            else:
+                qw2 = self.q.copy()
+                qw2[r, c] = flip(qw2[r, c])
+                acc2 = int_gemm(qx, qw2)
+                acc[lo:hi, r] = acc2[lo:hi, r]
+        y = linear_epilogue(acc, sx, self.s, self.b)
+        if fault is not None and fault["kind"] == "OUTPUT":
+            y[fault["row"], fault["col"]] = f32(fault["value"]) + self.b[fault["col"]]
+        if relu:
+            y = np.where(y > 0, y, f32(0.0)).astype(f32)
         y = y.reshape(shp[:-1] + (y.shape[-1],))
         if quantize_output:          # get_quantized_model.py:160-168 (Q/K/V)
             return quant_rows(y)
@@ -299,42 +324,68 @@ class OracleModel:
         self.gen_w = np.asarray(sd["generator.proj.weight"], f32)
         self.gen_b = np.asarray(sd["generator.proj.bias"], f32)
 
-    # -- sublayers ---------------------------------------------------------------------
-    def mha(self, lin, xq, xkv, mask):
-        """MultiHeadedAttention.forward (attention.py:39-67)."""
-        qq, sq = lin[0](xq, quantize_output=True)
-        qk, sk = lin[1](xkv, quantize_output=True)
-        qv, sv = lin[2](xkv, quantize_output=True)
-        ctx, _ = attention(qq, sq, qk, sk, qv, sv, mask, self.H)
-        return lin[3](ctx)
+    # -- fault injection ---------------------------------------------------------------
+    @staticmethod
+    def _lin_fault(fault, module, layer, linear, rows, n_out):
+        """The fault (qtx.fault.Fault-like dict) as a QLinear fault dict if it targets this
+        linear, else None.  Windows: INPUT16 columns, WEIGHT16 rows."""
+        if (fault is None or fault["module"] != module or fault["layer"] != layer
+                or fault["linear"] != linear):
+            return None
+        k = fault["kind"]
+        kind = "OUTPUT" if k.startswith("RANDOM") or k == "OUTPUT" else k
+        if kind in ("INPUT16", "WEIGHT16"):
+            lo, hi = fault["win_start"], fault["win_start"] + fault["win_len"]
+        else:
+            lo, hi = 0, (n_out if kind == "INPUT" else rows)
+        return dict(kind=kind, row=fault["row"], col=fault["col"], bit=fault.get("bit", 0),
+                    lo=lo, hi=hi, value=fault.get("value", 0.0))
 
-    def ffn(self, lp, x):
+    # -- sublayers ---------------------------------------------------------------------
+    def mha(self, lin, xq, xkv, mask, faults=(None,) * 4):
+        """MultiHeadedAttention.forward (attention.py:39-67)."""
+        qq, sq = lin[0](xq, quantize_output=True, fault=faults[0])
+        qk, sk = lin[1](xkv, quantize_output=True, fault=faults[1])
+        qv, sv = lin[2](xkv, quantize_output=True, fault=faults[2])
+        ctx, _ = attention(qq, sq, qk, sk, qv, sv, mask, self.H)
+        return lin[3](ctx, fault=faults[3])
+
+    def ffn(self, lp, x, faults=(None, None)):
         """PositionwiseFeedForward.forward (position_feed_forward.py:11-12)."""
-        return lp["w2"](lp["w1"](x, relu=True))
+        return lp["w2"](lp["w1"](x, relu=True, fault=faults[0]), fault=faults[1])
 
     # -- stacks ------------------------------------------------------------------------
-    def encode(self, x, src_mask):
-        """Encoder.forward (encoder.py:14-18, 29-32). x [B,S,512], src_mask [B,1,S]."""
+    def encode(self, x, src_mask, fault=None):
+        """Encoder.forward (encoder.py:14-18, 29-32). x [B,S,512], src_mask [B,1,S].
+        fault: optional dict (qtx.fault.Fault.as_dict()) with module 0."""
         x = np.asarray(x, f32)
         m = np.asarray(src_mask).reshape(x.shape[0], 1, -1)
-        for lp in self.enc:
+        rows = x.shape[0] * x.shape[1]
+        for L, lp in enumerate(self.enc):
+            lf = lambda lin, n=512: self._lin_fault(fault, 0, L, lin, rows, n)
             h = layer_norm(x, *lp["ln"][0])
-            x = x + self.mha(lp["attn"], h, h, m)
-            x = x + self.ffn(lp, layer_norm(x, *lp["ln"][1]))
+            x = x + self.mha(lp["attn"], h, h, m, [lf("Q"), lf("K"), lf("V"), lf("O")])
+            x = x + self.ffn(lp, layer_norm(x, *lp["ln"][1]),
+                             [lf("FFN1", lp["w1"].q.shape[0]), lf("FFN2")])
         return layer_norm(x, *self.enc_norm)
 
-    def decode(self, y, memory, src_mask, tgt_mask):
-        """Decoder.forward (decoder.py:13-16, 28-33). tgt_mask [1|B,T,T]."""
+    def decode(self, y, memory, src_mask, tgt_mask, fault=None):
+        """Decoder.forward (decoder.py:13-16, 28-33). tgt_mask [1|B,T,T].
+        fault: optional dict (qtx.fault.Fault.as_dict()) with module 1."""
         x = np.asarray(y, f32)
         B = x.shape[0]
         sm = np.asarray(src_mask).reshape(B, 1, -1)
         tm = np.broadcast_to(np.asarray(tgt_mask), (B,) + np.asarray(tgt_mask).shape[-2:])
-        for lp in self.dec:
+        rows, mrows = B * x.shape[1], B * np.asarray(memory).shape[1]
+        for L, lp in enumerate(self.dec):
+            lf = lambda lin, r=rows, n=512: self._lin_fault(fault, 1, L, lin, r, n)
             h = layer_norm(x, *lp["ln"][0])
-            x = x + self.mha(lp["self_attn"], h, h, tm)
+            x = x + self.mha(lp["self_attn"], h, h, tm, [lf("Q"), lf("K"), lf("V"), lf("O")])
             h = layer_norm(x, *lp["ln"][1])
-            x = x + self.mha(lp["src_attn"], h, memory, sm)
-            x = x + self.ffn(lp, layer_norm(x, *lp["ln"][2]))
+            x = x + self.mha(lp["src_attn"], h, memory, sm,
+                             [lf("CQ"), lf("CK", mrows), lf("CV", mrows), lf("CO")])
+            x = x + self.ffn(lp, layer_norm(x, *lp["ln"][2]),
+                             [lf("FFN1", rows, lp["w1"].q.shape[0]), lf("FFN2")])
         return layer_norm(x, *self.dec_norm)
 
     # -- host-side pieces of the decode loop ---------------------------------------------
@@ -362,7 +413,7 @@ class OracleModel:
         lp = z - lse[:, None]
         return lp.astype(f32), lp.argmax(axis=-1)
 
-    def greedy_decode(self, src, src_mask, max_len=72, start=0, kv_cache=True):
+    def greedy_decode(self, src, src_mask, max_len=72, start=0, kv_cache=True, fault=None):
         """Batched greedy decode (batch_output.py:659-673; B=1 form
         reference/onnx_reference_inference.py:622-646): fixed max_len-1 steps, no EOS exit.
 
@@ -371,7 +422,7 @@ class OracleModel:
         """
         src = np.asarray(src)
         B = src.shape[0]
-        memory = self.encode(self.embed(src, self.src_lut), src_mask)
+        memory = self.encode(self.embed(src, self.src_lut), src_mask, fault=fault)
         ys = np.full((B, 1), start, np.int64)
         if not kv_cache:
             for _ in range(max_len - 1):
