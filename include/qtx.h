@@ -113,14 +113,24 @@ int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t*
  *   WEIGHT16  as WEIGHT, the perturbation kept on rows win_start .. +win_len (<= 16)
  *   OUTPUT    the MatMul output (before bias) at (row, col) replaced by `value`
  *             (RANDOM: a random float; RANDOM_BITFLIP: a bit-flipped golden value)
+ * Attention MatMuls (QTX_LIN_QK / PV, decoder cross QTX_LIN_CQK / CPV; the reference's
+ * "FirstMatMul" / "SecondMatMul" campaign targets) on one (sentence b, head h), Sq query
+ * and Sk key rows per sentence:
+ *   QK  INPUT*:  q element  row = b*Sq + i, col = h*64 + d   (INPUT16 window: keys)
+ *       WEIGHT*: k element  row = b*Sk + j, col = h*64 + d   (WEIGHT16 window: query rows)
+ *       OUTPUT:  QK^T value row = b*Sq + i, col = h*Sk + j   (before the / 8 and the mask)
+ *   PV  INPUT*:  P*127 int  row = b*Sq + i, col = h*Sk + j   (INPUT16 window: head dims)
+ *       WEIGHT*: v element  row = b*Sk + j, col = h*64 + d   (WEIGHT16 window: query rows)
+ *       OUTPUT:  context    row = b*Sq + i, col = h*64 + d
  * Requires 8-bit weights. */
 typedef enum {
   QTX_FAULT_NONE = 0, QTX_FAULT_INPUT = 1, QTX_FAULT_WEIGHT = 2, QTX_FAULT_INPUT16 = 3,
   QTX_FAULT_WEIGHT16 = 4, QTX_FAULT_OUTPUT = 5
 } qtx_fault_kind;
 typedef enum {
-  QTX_LIN_Q = 0, QTX_LIN_K = 1, QTX_LIN_V = 2, QTX_LIN_O = 5, QTX_LIN_FFN1 = 6,
-  QTX_LIN_FFN2 = 7, QTX_LIN_CQ = 8, QTX_LIN_CK = 9, QTX_LIN_CV = 10, QTX_LIN_CO = 11
+  QTX_LIN_Q = 0, QTX_LIN_K = 1, QTX_LIN_V = 2, QTX_LIN_QK = 3, QTX_LIN_PV = 4, QTX_LIN_O = 5,
+  QTX_LIN_FFN1 = 6, QTX_LIN_FFN2 = 7, QTX_LIN_CQ = 8, QTX_LIN_CK = 9, QTX_LIN_CV = 10,
+  QTX_LIN_CO = 11, QTX_LIN_CQK = 12, QTX_LIN_CPV = 13
 } qtx_linear_id;
 typedef struct {
   int32_t kind;      /* qtx_fault_kind */

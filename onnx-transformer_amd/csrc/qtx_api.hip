@@ -523,16 +523,91 @@ FaultArgs fault_for(const qtx_fault* f, int module, int layer, GemmId gid, int M
   return fa;
 }
 
+// The fault as an AttnFault if it targets this layer's self (cross = false) or cross
+// attention MatMuls (see qtx.h for the index conventions).
+bool attn_fault_for(const qtx_fault* f, int module, int layer, bool cross, int Sq, int Sk,
+                    AttnFault& af) {
+  if (!f || f->kind == QTX_FAULT_NONE || f->module != module || f->layer != layer) return false;
+  const int lin = f->linear;
+  bool qk;
+  if (!cross && (lin == QTX_LIN_QK || lin == QTX_LIN_PV)) qk = lin == QTX_LIN_QK;
+  else if (cross && (lin == QTX_LIN_CQK || lin == QTX_LIN_CPV)) qk = lin == QTX_LIN_CQK;
+  else return false;
+  const bool in = f->kind == QTX_FAULT_INPUT || f->kind == QTX_FAULT_INPUT16;
+  const bool win = f->kind == QTX_FAULT_INPUT16 || f->kind == QTX_FAULT_WEIGHT16;
+  af = AttnFault{};
+  af.bit = f->bit;
+  af.value = f->value;
+  const long row = f->row, col = f->col;
+  if (f->kind == QTX_FAULT_OUTPUT) {
+    af.kind = qk ? AF_QK_OUTPUT : AF_PV_OUTPUT;
+    af.b = row / Sq; af.i = row % Sq;
+    if (qk) { af.h = col / Sk; af.j = col % Sk; } else { af.h = col / 64; af.d = col % 64; }
+    af.row0 = af.i; af.nrows = 1;
+    return true;
+  }
+  if (in) {
+    af.kind = qk ? AF_QK_INPUT : AF_PV_INPUT;
+    af.b = row / Sq; af.i = row % Sq;
+    if (qk) { af.h = col / 64; af.d = col % 64; } else { af.h = col / Sk; af.j = col % Sk; }
+    af.lo = win ? (int)f->win_start : 0;
+    af.hi = win ? (int)(f->win_start + f->win_len) : (qk ? Sk : 64);
+    af.row0 = af.i; af.nrows = 1;
+  } else {
+    af.kind = qk ? AF_QK_WEIGHT : AF_PV_WEIGHT;
+    af.b = row / Sk; af.j = row % Sk; af.h = col / 64; af.d = col % 64;
+    af.lo = win ? (int)f->win_start : 0;
+    af.hi = win ? (int)(f->win_start + f->win_len) : Sq;
+    af.row0 = af.lo; af.nrows = af.hi - af.lo;
+  }
+  return true;
+}
+
+// attention with an optional fault: fp32 context (+ the faulty rows recomputed), then the
+// per-token quantization of the O-projection input
+int attention_fault(const AttnArgs& a, const AttnFault& af, int M, int D, Scratch& s,
+                    hipStream_t st) {
+  HIPCHK(launch_attention(a, st));
+  HIPCHK(launch_attn_fault_rows(a, af, st));
+  RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+  return QTX_OK;
+}
+
 // Validates a fault against the shapes of its target MatMul (M token rows of the module,
 // Ms memory rows for the decoder's cross K/V); returns QTX_OK or an error code.
-int check_fault(const qtx_model* m, const qtx_fault* f, int module, long M, long Ms) {
+int check_fault(const qtx_model* m, const qtx_fault* f, int module, long B, long Sq, long Ss) {
   if (!f || f->kind == QTX_FAULT_NONE) return QTX_OK;
   const qtx_config& c = m->cfg;
+  const long M = B * Sq, Ms = B * Ss;
   if (!row_path(c)) return fail(QTX_E_UNSUPPORTED, "fault injection needs 8-bit weights");
   if (f->kind < 0 || f->kind > QTX_FAULT_OUTPUT) return fail(QTX_E_INVALID, "fault kind %d", f->kind);
   if (f->module != module) return fail(QTX_E_INVALID, "fault module %d", f->module);
   if (f->layer < 0 || f->layer >= c.n_layers) return fail(QTX_E_INVALID, "fault layer %d", f->layer);
   const int lin = f->linear;
+  const bool in_kind = f->kind == QTX_FAULT_INPUT || f->kind == QTX_FAULT_INPUT16;
+  const bool w_kind = f->kind == QTX_FAULT_WEIGHT || f->kind == QTX_FAULT_WEIGHT16;
+  const bool win = f->kind == QTX_FAULT_INPUT16 || f->kind == QTX_FAULT_WEIGHT16;
+  if ((in_kind || w_kind) && (f->bit < 0 || f->bit > 7)) return fail(QTX_E_INVALID, "fault bit %d", f->bit);
+  auto bad_idx = [&](long r, long nr, long cc, long nc) {
+    return fail(QTX_E_INVALID, "fault index (%ld, %ld) outside [%ld, %ld]", r, cc, nr, nc);
+  };
+  const long row = f->row, col = f->col;
+  const bool attn_self = lin == QTX_LIN_QK || lin == QTX_LIN_PV;
+  const bool attn_cross = lin == QTX_LIN_CQK || lin == QTX_LIN_CPV;
+  if (attn_self || attn_cross) {
+    if (attn_cross && module != 1) return fail(QTX_E_INVALID, "fault linear %d", lin);
+    const long sq = Sq, sk = attn_cross ? Ss : Sq, H = c.n_heads;
+    if (sk > 512) return fail(QTX_E_UNSUPPORTED, "attention fault with %ld keys", sk);
+    const bool qk = lin == QTX_LIN_QK || lin == QTX_LIN_CQK;
+    long nr, nc, wmax;
+    if (f->kind == QTX_FAULT_OUTPUT) { nr = B * sq; nc = qk ? H * sk : H * 64; wmax = 0; }
+    else if (in_kind) { nr = B * sq; nc = qk ? H * 64 : H * sk; wmax = qk ? sk : 64; }
+    else { nr = B * sk; nc = H * 64; wmax = sq; }
+    if (row < 0 || row >= nr || col < 0 || col >= nc) return bad_idx(row, nr, col, nc);
+    if (win && (f->win_len < 1 || f->win_len > 16 || f->win_start < 0 || f->win_start + f->win_len > wmax))
+      return fail(QTX_E_INVALID, "fault window [%ld, +%d) outside %ld", (long)f->win_start, f->win_len, wmax);
+    return QTX_OK;
+  }
   const bool enc_ok = lin == QTX_LIN_Q || lin == QTX_LIN_K || lin == QTX_LIN_V || lin == QTX_LIN_O ||
                       lin == QTX_LIN_FFN1 || lin == QTX_LIN_FFN2;
   const bool dec_ok = enc_ok || (lin >= QTX_LIN_CQ && lin <= QTX_LIN_CO);
@@ -540,15 +615,10 @@ int check_fault(const qtx_model* m, const qtx_fault* f, int module, long M, long
   const long rows = (lin == QTX_LIN_CK || lin == QTX_LIN_CV) ? Ms : M;
   const long K = lin == QTX_LIN_FFN2 ? c.d_ff : c.d_model;
   const long N = lin == QTX_LIN_FFN1 ? c.d_ff : c.d_model;
-  const bool in_kind = f->kind == QTX_FAULT_INPUT || f->kind == QTX_FAULT_INPUT16;
-  const bool w_kind = f->kind == QTX_FAULT_WEIGHT || f->kind == QTX_FAULT_WEIGHT16;
-  if ((in_kind || w_kind) && (f->bit < 0 || f->bit > 7)) return fail(QTX_E_INVALID, "fault bit %d", f->bit);
-  if (in_kind && (f->row < 0 || f->row >= rows || f->col < 0 || f->col >= K))
-    return fail(QTX_E_INVALID, "input fault index (%ld, %ld) outside [%ld, %ld]", (long)f->row, (long)f->col, rows, K);
-  if (w_kind && (f->row < 0 || f->row >= N || f->col < 0 || f->col >= K))
-    return fail(QTX_E_INVALID, "weight fault index (%ld, %ld) outside [%ld, %ld]", (long)f->row, (long)f->col, N, K);
-  if (f->kind == QTX_FAULT_OUTPUT && (f->row < 0 || f->row >= rows || f->col < 0 || f->col >= N))
-    return fail(QTX_E_INVALID, "output fault index (%ld, %ld) outside [%ld, %ld]", (long)f->row, (long)f->col, rows, N);
+  if (in_kind && (row < 0 || row >= rows || col < 0 || col >= K)) return bad_idx(row, rows, col, K);
+  if (w_kind && (row < 0 || row >= N || col < 0 || col >= K)) return bad_idx(row, N, col, K);
+  if (f->kind == QTX_FAULT_OUTPUT && (row < 0 || row >= rows || col < 0 || col >= N))
+    return bad_idx(row, rows, col, N);
   if (f->kind == QTX_FAULT_INPUT16 &&
       (f->win_len < 1 || f->win_len > 16 || f->win_start < 0 || f->win_start + f->win_len > N))
     return fail(QTX_E_INVALID, "INPUT16 window");
@@ -583,9 +653,14 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
     AttnArgs a = attn_args(s, B, S, S, S);
     a.mask = mask; a.m_bs = S; a.m_is = 0;
     a.c_ld = D;
-    const hipError_t ea = getenv("QTX_NO_ATTN_ENCQ") ? hipErrorNotSupported
-                                                     : launch_attention_encq(a, s.a8, s.sa, st);
-    if (ea == hipErrorNotSupported) {    // other shapes: fp32 context + quantization kernel
+    AttnFault af;
+    const hipError_t ea = attn_fault_for(f, 0, l, false, S, S, af)
+                              ? hipErrorNotSupported
+                              : (getenv("QTX_NO_ATTN_ENCQ") ? hipErrorNotSupported
+                                                            : launch_attention_encq(a, s.a8, s.sa, st));
+    if (attn_fault_for(f, 0, l, false, S, S, af)) {
+      RC(attention_fault(a, af, M, D, s, st));
+    } else if (ea == hipErrorNotSupported) {  // other shapes: fp32 context + quantization
       HIPCHK(launch_attention(a, st));
       RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
     } else {
@@ -934,7 +1009,7 @@ int32_t qtx_encoder_forward_fault(const qtx_model* m, const float* x, const uint
   if (!m || !x || !src_mask || !out || !ws) return fail(QTX_E_INVALID, "null argument");
   if (B <= 0 || S <= 0 || S > 512) return fail(QTX_E_INVALID, "bad shape B=%d S=%d", B, S);
   if (ws_bytes < enc_ws(m->cfg, B, S)) return fail(QTX_E_WORKSPACE, "workspace too small");
-  RC(check_fault(m, f, 0, (long)B * S, 0));
+  RC(check_fault(m, f, 0, B, S, 0));
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
   Scratch s = carve_scratch(ar, m->cfg, (long)B * S);
@@ -957,7 +1032,7 @@ int32_t qtx_decoder_forward_fault(const qtx_model* m, const float* y, const floa
   if (B <= 0 || T <= 0 || S <= 0 || T > 512 || S > 512)
     return fail(QTX_E_INVALID, "bad shape B=%d T=%d S=%d", B, T, S);
   if (ws_bytes < dec_ws(m->cfg, B, T, S)) return fail(QTX_E_WORKSPACE, "workspace too small");
-  RC(check_fault(m, f, 1, (long)B * T, (long)B * S));
+  RC(check_fault(m, f, 1, B, T, S));
   hipStream_t st = (hipStream_t)stream;
   const qtx_config& c = m->cfg;
   const int D = c.d_model, M = B * T;
@@ -989,21 +1064,30 @@ int32_t qtx_decoder_forward_fault(const qtx_model* m, const float* y, const floa
     AttnArgs a = attn_args(s, B, T, T, T);
     a.mask = tgt_mask; a.m_bs = tm_bs; a.m_is = T;
     a.c_ld = D;
-    const hipError_t ea = getenv("QTX_NO_ATTN_ENCQ") ? hipErrorNotSupported
-                                                     : launch_attention_encq(a, s.a8, s.sa, st);
-    if (ea == hipErrorNotSupported) {    // other shapes: fp32 context + quantization kernel
-      HIPCHK(launch_attention(a, st));
-      RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+    AttnFault af;
+    if (attn_fault_for(f, 1, l, false, T, T, af)) {
+      RC(attention_fault(a, af, M, D, s, st));
     } else {
-      HIPCHK(ea);
+      const hipError_t ea = getenv("QTX_NO_ATTN_ENCQ") ? hipErrorNotSupported
+                                                       : launch_attention_encq(a, s.a8, s.sa, st);
+      if (ea == hipErrorNotSupported) {  // other shapes: fp32 context + quantization kernel
+        HIPCHK(launch_attention(a, st));
+        RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+      } else {
+        HIPCHK(ea);
+      }
     }
     RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st, fa(G_O)));
     RC(row_quant(L.cq, s.a8, s.sa, M, s.q8, s.sq, st, fa(G_CQ)));
     a = attn_args(s, B, T, S, S);
     a.k = x.k8[l]; a.sk = x.sk[l]; a.v = x.v8[l]; a.sv = x.sv[l];
     a.mask = src_mask; a.m_bs = S; a.m_is = 0;
-    HIPCHK(launch_attention(a, st));
-    RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+    if (attn_fault_for(f, 1, l, true, T, S, af)) {
+      RC(attention_fault(a, af, M, D, s, st));
+    } else {
+      HIPCHK(launch_attention(a, st));
+      RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+    }
     RC(row_res_ln(L.co, s.a8, s.sa, M, s.x, L.ln[2], s.a8, s.sa, nullptr, st, fa(G_CO)));
     RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1)));
     if (l + 1 < NL)
@@ -1061,7 +1145,7 @@ int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
   if (f && f->kind != QTX_FAULT_NONE && f->module != 0)
     return fail(QTX_E_UNSUPPORTED, "greedy decode takes encoder faults (decoder faults: "
                                    "qtx_decoder_forward_fault on the step's prefix)");
-  RC(check_fault(m, f, 0, (long)B * S, 0));
+  RC(check_fault(m, f, 0, B, S, 0));
   hipStream_t st = (hipStream_t)stream;
   const int D = c.d_model;
   Arena ar;

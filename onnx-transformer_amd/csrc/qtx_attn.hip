@@ -463,3 +463,97 @@ hipError_t launch_attention_encq(const AttnArgs& a, int8_t* ctx8, float* sctx, h
 }
 
 }  // namespace qtx
+
+namespace qtx {
+
+// =====================================================================================
+// k_attn_fault_rows: fault injection into the attention MatMuls (QK^T "FirstMatMul", PV
+// "SecondMatMul": the reference's campaign targets input/*/matmul_{8L+3,8L+4}.json etc.).
+// Recomputes the context of the affected query rows of ONE (sentence, head) from the int8
+// Q/K/V with the fault applied, in the canonical order (oracle attention_scores /
+// softmax_quant / attention_pv), overwriting their fp32 context (the unfused path's ctx,
+// quantized per token afterwards).  One wave per affected row.
+//   AF_QK_INPUT   q[row i][d] bit-flipped: acc[i][j] += dq * k[j][d] for keys j in [lo, hi)
+//   AF_QK_WEIGHT  k[j0][d] bit-flipped:     acc[i][j0] += q[i][d] * dk for rows i in [lo, hi)
+//   AF_PV_INPUT   P*127 int at (i, j0) bit-flipped: the PV chain of row i uses the flipped P
+//                 for dims d in [lo, hi)
+//   AF_PV_WEIGHT  v[j0][d0] bit-flipped: the PV chain of dim d0 uses it for rows in [lo, hi)
+// =====================================================================================
+__global__ __launch_bounds__(64) void k_attn_fault_rows(AttnArgs a, AttnFault f) {
+  __shared__ float Ps[512];
+  __shared__ float Pf[512];
+  const int lane = threadIdx.x;
+  const int b = f.b, h = f.h, Sk = a.Sk;
+  const int i = f.row0 + blockIdx.x;                 // the query row of this wave
+  const int hoff = 64 * h;
+  const int8_t* qrow = a.q + b * a.q_bs + (long)i * a.q_ld + hoff;
+  const float sqi = a.sq[b * a.sq_bs + i];
+  auto flip = [&](int8_t v) { return (int)(int8_t)(v ^ (1 << f.bit)); };
+  // ---- scores of the lane's keys j = lane + 64 t -------------------------------------
+  float x[8];
+  float m = -3.0e38f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int j = lane + 64 * t;
+    x[t] = -3.0e38f;
+    if (j < Sk) {
+      const int8_t* krow = a.k + b * a.k_bs + (long)j * a.k_ld + hoff;
+      int acc = 0;
+      for (int d = 0; d < 64; ++d) acc += (int)qrow[d] * (int)krow[d];
+      if (f.kind == AF_QK_INPUT && i == f.i && j >= f.lo && j < f.hi)
+        acc += (flip(qrow[f.d]) - (int)qrow[f.d]) * (int)krow[f.d];
+      if (f.kind == AF_QK_WEIGHT && j == f.j && i >= f.lo && i < f.hi)
+        acc += (int)qrow[f.d] * (flip(krow[f.d]) - (int)krow[f.d]);
+      float sc = (((float)acc * sqi) * a.sk[b * a.sk_bs + j]) / 8.0f;
+      if (f.kind == AF_QK_OUTPUT && i == f.i && j == f.j) sc = f.value / 8.0f;
+      const bool keep = !a.mask || a.mask[b * a.m_bs + (long)i * a.m_is + j] != 0;
+      x[t] = keep ? sc : -1.0e9f;
+      m = fmaxf(m, x[t]);
+    }
+  }
+  m = wave_max(m);
+  // ---- softmax: lane-split partial sums (start 0), canonical butterfly ------------------
+  float part = 0.0f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int j = lane + 64 * t;
+    x[t] = j < Sk ? qexp(x[t] - m) : 0.0f;
+    if (64 * t < Sk) part = part + x[t];
+  }
+  const float den = wave_sum(part);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int j = lane + 64 * t;
+    if (j < Sk) {
+      const float n = rintf((x[t] / den) * 127.0f);
+      Ps[j] = n / 127.0f;
+      Pf[j] = Ps[j];
+      if (f.kind == AF_PV_INPUT && i == f.i && j == f.j)
+        Pf[j] = (float)flip((int8_t)(int)n) / 127.0f;
+    }
+  }
+  __syncthreads();
+  // ---- PV: lane = dim d, sequential fma chain over the keys ----------------------------
+  const int d = lane;
+  const bool pin = f.kind == AF_PV_INPUT && i == f.i && d >= f.lo && d < f.hi;
+  const bool vw = f.kind == AF_PV_WEIGHT && d == f.d && i >= f.lo && i < f.hi;
+  float acc = 0.0f;
+  for (int j = 0; j < Sk; ++j) {
+    const int8_t v8 = a.v[b * a.v_bs + (long)j * a.v_ld + hoff + d];
+    const int vv = (vw && j == f.j) ? flip(v8) : (int)v8;
+    const float vb = (float)vv * a.sv[b * a.sv_bs + j];
+    acc = fmaf(pin ? Pf[j] : Ps[j], vb, acc);
+  }
+  if (f.kind == AF_PV_OUTPUT && i == f.i && d == f.d) acc = f.value;
+  a.ctx[b * a.c_bs + (long)i * a.c_ld + hoff + d] = acc;
+}
+
+hipError_t launch_attn_fault_rows(const AttnArgs& a, const AttnFault& f, hipStream_t st) {
+  if (a.Sk <= 0 || a.Sk > 512 || f.nrows <= 0 || f.b < 0 || f.b >= a.B || f.h < 0 ||
+      f.h >= a.H || f.row0 < 0 || f.row0 + f.nrows > a.Sq)
+    return hipErrorInvalidValue;
+  k_attn_fault_rows<<<dim3(f.nrows), dim3(64), 0, st>>>(a, f);
+  return hipGetLastError();
+}
+
+}  // namespace qtx

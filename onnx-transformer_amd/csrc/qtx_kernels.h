@@ -91,6 +91,19 @@ struct AttnArgs {
   const int* qpos_dev;                      // if set, query i's mask row = *qpos_dev + i
 };
 
+// Fault in an attention MatMul of one (sentence b, head h) (k_attn_fault_rows): the
+// affected query rows row0 .. row0+nrows-1 are recomputed with it.  i / j / d: the faulty
+// element's query row, key, head dim; [lo, hi): the window (keys for AF_QK_INPUT, rows for
+// the *_WEIGHT kinds, dims for AF_PV_INPUT).
+//   AF_QK_OUTPUT / AF_PV_OUTPUT: the MatMul output at (i, j) / (i, d) replaced by value
+enum { AF_QK_INPUT = 1, AF_QK_WEIGHT = 2, AF_PV_INPUT = 3, AF_PV_WEIGHT = 4, AF_QK_OUTPUT = 5,
+       AF_PV_OUTPUT = 6 };
+struct AttnFault {
+  int kind, bit, b, h, i, j, d, lo, hi, row0, nrows;
+  float value;
+};
+hipError_t launch_attn_fault_rows(const AttnArgs& a, const AttnFault& f, hipStream_t st);
+
 // Row-complete int8 GEMM (large M, 8-bit weights, N % 512 == 0, K % 64 == 0): each
 // workgroup owns 128 rows x one 512-wide column tile, so epilogues that need a whole
 // 512-wide row segment run in the same kernel.  y = ((float(acc) * sa[m]) * sw[n]) + b[n]:

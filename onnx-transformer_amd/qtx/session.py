@@ -161,8 +161,10 @@ def run_module(module, input_values, module_filepath=None, module_weight_dict=No
             if inject_parameters["inject_type"] == "RANDOM_BITFLIP":
                 raise ValueError("RANDOM_BITFLIP needs the golden MatMul output: draw the "
                                  "fault with qtx.fault.random_fault(golden_output=...)")
+            B, Sq = _shape(x)[:2]
+            Sk = _shape(input_values["global_in_1"])[1] if lin in ("CQK", "CPV") else Sq
             flt = F.from_inject_parameters(dict(inject_parameters, targetted_module=kind), rows,
-                                           rng, model.cfg.n_layers, golden)
+                                           rng, model.cfg.n_layers, golden, (B, Sq, Sk))
         weight_dict["qtx_fault"] = flt
     out = fn(model, input_values, flt).cpu().numpy()
     weight_dict["global_out"] = out

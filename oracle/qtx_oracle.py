@@ -281,12 +281,58 @@ def merge_heads(x):
     return x.transpose(0, 2, 1, 3).reshape(B, S, H * dk)
 
 
-def attention(qq, sq, qk, sk, qv, sv, mask, H=8):
-    """Quantized Q/K/V [B,S,512] int8 + per-token scales -> ctx [B,Sq,512] f32, P ints."""
+def _flip8(v, bit):
+    """flip_int8_bit (inject_utils/layers.py:62-69) on int8 storage."""
+    return np.int8(np.uint8(np.int8(v).view(np.uint8) ^ (1 << int(bit))).view(np.int8))
+
+
+def attention(qq, sq, qk, sk, qv, sv, mask, H=8, fault=None):
+    """Quantized Q/K/V [B,S,512] int8 + per-token scales -> ctx [B,Sq,512] f32, P ints.
+
+    fault (fault-injection runs, one (sentence b, head h)): dict with kind QK_INPUT /
+    QK_WEIGHT / QK_OUTPUT / PV_INPUT / PV_WEIGHT / PV_OUTPUT and b, h, i, j, d, lo, hi,
+    bit, value (the conventions of include/qtx.h): a flipped q / k element changes the
+    exact int QK^T accumulators (INPUT: keys lo..hi of row i, WEIGHT: rows lo..hi of key
+    j); a flipped P*127 int / v element is used by the PV chain (INPUT: dims lo..hi of row
+    i, WEIGHT: rows lo..hi of dim d); OUTPUT replaces the QK^T value (before / 8 and the
+    mask) or the context value."""
     q4, k4, v4 = split_heads(qq, H), split_heads(qk, H), split_heads(qv, H)
-    scores = attention_scores(q4, sq, k4, sk, mask)
+    if fault is None:
+        scores = attention_scores(q4, sq, k4, sk, mask)
+        qp = softmax_quant(scores)
+        ctx = attention_pv(qp, v4, sv)
+        return merge_heads(ctx), qp
+    kind, b, h = fault["kind"], fault["b"], fault["h"]
+    i, j, d, lo, hi, bit = (fault[k] for k in ("i", "j", "d", "lo", "hi", "bit"))
+    acc = np.einsum("bhid,bhjd->bhij", q4.astype(np.int64), k4.astype(np.int64))
+    if kind == "QK_INPUT":
+        dq = int(_flip8(q4[b, h, i, d], bit)) - int(q4[b, h, i, d])
+        acc[b, h, i, lo:hi] += dq * k4[b, h, lo:hi, d].astype(np.int64)
+    elif kind == "QK_WEIGHT":
+        dk = int(_flip8(k4[b, h, j, d], bit)) - int(k4[b, h, j, d])
+        acc[b, h, lo:hi, j] += q4[b, h, lo:hi, d].astype(np.int64) * dk
+    s = acc.astype(np.int32).astype(f32)
+    s = s * np.asarray(sq, f32)[:, None, :, None]
+    s = s * np.asarray(sk, f32)[:, None, None, :]
+    s = s / f32(8.0)
+    if kind == "QK_OUTPUT":
+        s[b, h, i, j] = f32(fault["value"]) / f32(8.0)
+    keep = np.broadcast_to(np.asarray(mask) != 0, (q4.shape[0], q4.shape[2], k4.shape[2]))
+    scores = np.where(keep[:, None], s, MASK_FILL).astype(f32)
     qp = softmax_quant(scores)
     ctx = attention_pv(qp, v4, sv)
+    if kind == "PV_INPUT":
+        qp2 = qp[b:b + 1, h:h + 1].copy()
+        qp2[0, 0, i, j] = _flip8(qp2[0, 0, i, j], bit)
+        c2 = attention_pv(qp2, v4[b:b + 1, h:h + 1], np.asarray(sv)[b:b + 1])
+        ctx[b, h, i, lo:hi] = c2[0, 0, i, lo:hi]
+    elif kind == "PV_WEIGHT":
+        v2 = v4[b:b + 1, h:h + 1].copy()
+        v2[0, 0, j, d] = _flip8(v2[0, 0, j, d], bit)
+        c2 = attention_pv(qp[b:b + 1, h:h + 1], v2, np.asarray(sv)[b:b + 1])
+        ctx[b, h, lo:hi, d] = c2[0, 0, lo:hi, d]
+    elif kind == "PV_OUTPUT":
+        ctx[b, h, i, d] = f32(fault["value"])
     return merge_heads(ctx), qp
 
 
@@ -342,12 +388,49 @@ class OracleModel:
                     lo=lo, hi=hi, value=fault.get("value", 0.0))
 
     # -- sublayers ---------------------------------------------------------------------
-    def mha(self, lin, xq, xkv, mask, faults=(None,) * 4):
+    @staticmethod
+    def _attn_fault(fault, module, layer, qk_name, pv_name, Sq, Sk):
+        """The fault as an oracle attention() fault dict if it targets this attention's
+        QK^T (qk_name) or PV (pv_name) MatMul, else None (index conventions: qtx.h)."""
+        if (fault is None or fault["module"] != module or fault["layer"] != layer
+                or fault["linear"] not in (qk_name, pv_name)):
+            return None
+        qk = fault["linear"] == qk_name
+        k = fault["kind"]
+        out = k.startswith("RANDOM") or k == "OUTPUT"
+        inp = k.startswith("INPUT")
+        win = k.endswith("16")
+        r, c = fault["row"], fault["col"]
+        f = dict(bit=fault.get("bit", 0), value=fault.get("value", 0.0), i=0, j=0, d=0, lo=0, hi=0)
+        if out or inp:
+            f["b"], f["i"] = divmod(r, Sq)
+            if qk and inp:
+                f["h"], f["d"] = divmod(c, 64)
+            elif qk or inp:
+                f["h"], f["j"] = divmod(c, Sk)
+            else:
+                f["h"], f["d"] = divmod(c, 64)
+        else:
+            f["b"], f["j"] = divmod(r, Sk)
+            f["h"], f["d"] = divmod(c, 64)
+        if out:
+            f["kind"] = "QK_OUTPUT" if qk else "PV_OUTPUT"
+        elif inp:
+            f["kind"] = "QK_INPUT" if qk else "PV_INPUT"
+            f["lo"], f["hi"] = ((fault["win_start"], fault["win_start"] + fault["win_len"]) if win
+                                else (0, Sk if qk else 64))
+        else:
+            f["kind"] = "QK_WEIGHT" if qk else "PV_WEIGHT"
+            f["lo"], f["hi"] = ((fault["win_start"], fault["win_start"] + fault["win_len"]) if win
+                                else (0, Sq))
+        return f
+
+    def mha(self, lin, xq, xkv, mask, faults=(None,) * 4, attn_fault=None):
         """MultiHeadedAttention.forward (attention.py:39-67)."""
         qq, sq = lin[0](xq, quantize_output=True, fault=faults[0])
         qk, sk = lin[1](xkv, quantize_output=True, fault=faults[1])
         qv, sv = lin[2](xkv, quantize_output=True, fault=faults[2])
-        ctx, _ = attention(qq, sq, qk, sk, qv, sv, mask, self.H)
+        ctx, _ = attention(qq, sq, qk, sk, qv, sv, mask, self.H, fault=attn_fault)
         return lin[3](ctx, fault=faults[3])
 
     def ffn(self, lp, x, faults=(None, None)):
@@ -364,7 +447,9 @@ class OracleModel:
         for L, lp in enumerate(self.enc):
             lf = lambda lin, n=512: self._lin_fault(fault, 0, L, lin, rows, n)
             h = layer_norm(x, *lp["ln"][0])
-            x = x + self.mha(lp["attn"], h, h, m, [lf("Q"), lf("K"), lf("V"), lf("O")])
+            S = x.shape[1]
+            x = x + self.mha(lp["attn"], h, h, m, [lf("Q"), lf("K"), lf("V"), lf("O")],
+                             self._attn_fault(fault, 0, L, "QK", "PV", S, S))
             x = x + self.ffn(lp, layer_norm(x, *lp["ln"][1]),
                              [lf("FFN1", lp["w1"].q.shape[0]), lf("FFN2")])
         return layer_norm(x, *self.enc_norm)
@@ -380,10 +465,13 @@ class OracleModel:
         for L, lp in enumerate(self.dec):
             lf = lambda lin, r=rows, n=512: self._lin_fault(fault, 1, L, lin, r, n)
             h = layer_norm(x, *lp["ln"][0])
-            x = x + self.mha(lp["self_attn"], h, h, tm, [lf("Q"), lf("K"), lf("V"), lf("O")])
+            T, S = x.shape[1], np.asarray(memory).shape[1]
+            x = x + self.mha(lp["self_attn"], h, h, tm, [lf("Q"), lf("K"), lf("V"), lf("O")],
+                             self._attn_fault(fault, 1, L, "QK", "PV", T, T))
             h = layer_norm(x, *lp["ln"][1])
             x = x + self.mha(lp["src_attn"], h, memory, sm,
-                             [lf("CQ"), lf("CK", mrows), lf("CV", mrows), lf("CO")])
+                             [lf("CQ"), lf("CK", mrows), lf("CV", mrows), lf("CO")],
+                             self._attn_fault(fault, 1, L, "CQK", "CPV", T, S))
             x = x + self.ffn(lp, layer_norm(x, *lp["ln"][2]),
                              [lf("FFN1", rows, lp["w1"].q.shape[0]), lf("FFN2")])
         return layer_norm(x, *self.dec_norm)

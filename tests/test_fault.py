@@ -23,17 +23,20 @@ def test_matmul_names():
     assert F.matmul_target("MatMul_22", "Decoder") == (1, 0, "FFN1")     # matmul_22.json
     assert F.matmul_target("MatMul_23", "Decoder") == (1, 0, "FFN2")     # matmul_23.json
     assert F.matmul_target("MatMul_82", "Decoder") == (1, 5, "FFN1")
-    for bad in ("MatMul_3", "MatMul_4", "Add_3"):
+    assert F.matmul_target("MatMul_3", "Encoder") == (0, 0, "QK")       # matmul_3.json
+    assert F.matmul_target("MatMul_12", "Encoder") == (0, 1, "PV")
+    for bad in ("Add_3", "MatMul_48"):
         with pytest.raises(ValueError):
             F.matmul_target(bad, "Encoder")
-    for bad in ("MatMul_15", "MatMul_16", "MatMul_19", "MatMul_20"):      # QK^T / PV
-        with pytest.raises(ValueError):
-            F.matmul_target(bad, "Decoder")
+    assert F.matmul_target("MatMul_15", "Decoder") == (1, 0, "QK")       # matmul_15.json
+    assert F.matmul_target("MatMul_16", "Decoder") == (1, 0, "PV")
+    assert F.matmul_target("MatMul_19", "Decoder") == (1, 0, "CQK")      # matmul_19.json
+    assert F.matmul_target("MatMul_20", "Decoder") == (1, 0, "CPV")
 
 
 def test_reference_target_files_map():
-    """Every target of the reference's campaign files maps to a (module, layer, linear)
-    or is a non-QuantLinear MatMul (QK^T / PV)."""
+    """Every target of the reference's campaign files (QK^T, PV, FFN1, FFN2 per layer)
+    maps to the matching (module, layer, target)."""
     import glob
     import json
     import os
@@ -44,15 +47,13 @@ def test_reference_target_files_map():
     for mod in ("encoder", "decoder"):
         for p in glob.glob(f"{d}/{mod}/matmul_*.json"):
             j = json.load(open(p))
-            kind = j["module"].split("/")[1]          # FirstFC / SecondFC / *MatMul
-            if kind.endswith("FC"):
-                _, _, lin = F.matmul_target(j["target_layer"], j["module"])
-                assert lin == ("FFN1" if kind == "FirstFC" else "FFN2")
-                n += 1
-            else:                                     # attention QK^T / PV: not QuantLinears
-                with pytest.raises(ValueError):
-                    F.matmul_target(j["target_layer"], j["module"])
-    assert n == 24
+            kind = j["module"].split("/")[1]          # FirstFC / SecondFC / First|SecondMatMul
+            _, _, lin = F.matmul_target(j["target_layer"], j["module"])
+            want = {"FirstFC": ("FFN1",), "SecondFC": ("FFN2",), "FirstMatMul": ("QK", "CQK"),
+                    "SecondMatMul": ("PV", "CPV")}[kind]
+            assert lin in want, (p, lin)
+            n += 1
+    assert n == 24 + 36
 
 
 def test_random_fault_draws():
@@ -218,3 +219,66 @@ def test_run_module_inject_parameters(torch_gpu, gpu_model, oracle_model, golden
     assert (f.module, f.layer, f.linear, f.bit) == (0, 0, "FFN1", 7)
     ref = oracle_model.encode(golden_model["enc_in"], golden_model["src_mask"], fault=f.as_dict())
     np.testing.assert_array_equal(outs["global_out"], ref)
+
+
+ATTN_CASES = [("INPUT", "QK"), ("INPUT16", "QK"), ("WEIGHT", "QK"), ("WEIGHT16", "QK"),
+              ("RANDOM", "QK"), ("INPUT", "PV"), ("INPUT16", "PV"), ("WEIGHT", "PV"),
+              ("WEIGHT16", "PV"), ("RANDOM", "PV")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,linear", ATTN_CASES)
+def test_encoder_attention_fault_matches_oracle(torch_gpu, gpu_model, oracle_model, kind, linear):
+    torch = torch_gpu
+    B, S = 3, 24
+    src, m, x = _enc_inputs(oracle_model, B, S, 21)
+    rng = np.random.default_rng(abs(hash((kind, linear))) % 2**32)
+    f = F.random_attn_fault(rng, kind, 0, int(rng.integers(6)), linear, B, S, S, bit=7)
+    if kind == "RANDOM":
+        f.value = 37.25
+    out = gpu_model.encode(torch.from_numpy(x).cuda(),
+                           torch.from_numpy(m.reshape(B, S).astype(np.uint8)).cuda(),
+                           fault=f).cpu().numpy()
+    np.testing.assert_array_equal(out, oracle_model.encode(x, m, fault=f.as_dict()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,linear", [("INPUT", "CQK"), ("WEIGHT16", "CPV"), ("RANDOM", "CPV"),
+                                         ("WEIGHT", "QK"), ("INPUT16", "PV")])
+def test_decoder_attention_fault_matches_oracle(torch_gpu, gpu_model, oracle_model, kind, linear):
+    torch = torch_gpu
+    B, S, T = 2, 20, 6
+    src, m, x = _enc_inputs(oracle_model, B, S, 22)
+    rng = np.random.default_rng(8)
+    memory = oracle_model.encode(x, m)
+    y = oracle_model.embed(rng.integers(4, 4444, (B, T)), oracle_model.tgt_lut)
+    tm = np.tril(np.ones((1, T, T), np.uint8))
+    Sk = S if linear.startswith("C") else T
+    f = F.random_attn_fault(rng, kind, 1, int(rng.integers(6)), linear, B, T, Sk, bit=6)
+    if kind == "RANDOM":
+        f.value = -9.5
+    T_ = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    out = gpu_model.decode(T_(y), T_(memory), T_(m.reshape(B, S).astype(np.uint8)),
+                           T_(tm[0]), fault=f).cpu().numpy()
+    np.testing.assert_array_equal(out, oracle_model.decode(y, memory, m, tm, fault=f.as_dict()))
+
+
+def test_oracle_attention_fault_semantics():
+    """Oracle attention with a QK^T INPUT fault over all keys == attention on the flipped q."""
+    rng = np.random.default_rng(4)
+    B, S = 2, 9
+    q, k, v = (rng.integers(-127, 128, (B, S, 512)).astype(np.int8) for _ in range(3))
+    sq, sk, sv = (rng.uniform(0.002, 0.03, (B, S)).astype(f32) for _ in range(3))
+    mask = np.ones((B, 1, S), np.uint8)
+    q2 = q.copy()
+    q2[1, 4, 3 * 64 + 10] = O._flip8(q2[1, 4, 3 * 64 + 10], 7)
+    want, _ = O.attention(q2, sq, k, sk, v, sv, mask)
+    got, _ = O.attention(q, sq, k, sk, v, sv, mask, fault=dict(
+        kind="QK_INPUT", b=1, h=3, i=4, j=0, d=10, lo=0, hi=S, bit=7, value=0.0))
+    np.testing.assert_array_equal(got, want)
+    v2 = v.copy()
+    v2[0, 5, 2 * 64 + 7] = O._flip8(v2[0, 5, 2 * 64 + 7], 6)
+    want, _ = O.attention(q, sq, k, sk, v2, sv, mask)
+    got, _ = O.attention(q, sq, k, sk, v, sv, mask, fault=dict(
+        kind="PV_WEIGHT", b=0, h=2, i=0, j=5, d=7, lo=0, hi=S, bit=6, value=0.0))
+    np.testing.assert_array_equal(got, want)
