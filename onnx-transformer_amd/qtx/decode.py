@@ -28,6 +28,37 @@ def greedy_decode(model: QtxModel, src, src_mask, max_len: int, start_symbol: in
     return ys.to(src_t.device)
 
 
+def greedy_decode_fault(model: QtxModel, src, src_mask, max_len: int, start_symbol: int = 0,
+                        fault=None, target_inference_number: int = 1):
+    """Greedy decode with one injected fault, the reference campaign's loop
+    (parallelized_inject_onnx_transformer.py:536-720): an encoder fault corrupts the single
+    encoder run (memory); a decoder fault corrupts only the decoder run of step
+    ``target_inference_number - 1`` — every step recomputes the whole prefix, as the
+    reference does, so the faulty step changes that step's token and nothing else directly.
+    src / src_mask as greedy_decode; returns ys int64 [B, max_len] (numpy)."""
+    import torch
+    src = np.ascontiguousarray(np.asarray(src), np.int64)
+    B, S = src.shape
+    dev = model.device
+    srcd = torch.from_numpy(src).to(dev)
+    md = to_u8_mask(src_mask, dev).reshape(B, S)
+    enc_fault = fault if fault is not None and fault.module == 0 else None
+    dec_fault = fault if fault is not None and fault.module == 1 else None
+    if dec_fault is None:                       # KV-cached fused decode, faulty encoder
+        return model.greedy(srcd, md, max_len=max_len, start=start_symbol,
+                            fault=enc_fault).cpu().numpy()
+    memory = model.encode(model.embed(srcd, "src"), md)
+    ys = torch.full((B, 1), int(start_symbol), dtype=torch.int64, device=dev)
+    for i in range(max_len - 1):
+        T = ys.shape[1]
+        tm = torch.tril(torch.ones((T, T), dtype=torch.uint8, device=dev))
+        out = model.decode(model.embed(ys, "tgt"), memory, md, tm,
+                           fault=dec_fault if i == target_inference_number - 1 else None)
+        _, nxt = model.generator(out[:, -1].contiguous(), want_logp=False)
+        ys = torch.cat([ys, nxt[:, None]], dim=1)
+    return ys.cpu().numpy()
+
+
 def make_src_mask(src, pad: int = PAD):
     """Batch.src_mask = (src != pad).unsqueeze(-2)   (batch.py:7)."""
     return (np.asarray(src) != pad)[:, None, :]

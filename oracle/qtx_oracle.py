@@ -501,7 +501,8 @@ class OracleModel:
         lp = z - lse[:, None]
         return lp.astype(f32), lp.argmax(axis=-1)
 
-    def greedy_decode(self, src, src_mask, max_len=72, start=0, kv_cache=True, fault=None):
+    def greedy_decode(self, src, src_mask, max_len=72, start=0, kv_cache=True, fault=None,
+                      fault_step=0):
         """Batched greedy decode (batch_output.py:659-673; B=1 form
         reference/onnx_reference_inference.py:622-646): fixed max_len-1 steps, no EOS exit.
 
@@ -510,13 +511,18 @@ class OracleModel:
         """
         src = np.asarray(src)
         B = src.shape[0]
-        memory = self.encode(self.embed(src, self.src_lut), src_mask, fault=fault)
+        enc_fault = fault if fault is not None and fault["module"] == 0 else None
+        dec_fault = fault if fault is not None and fault["module"] == 1 else None
+        memory = self.encode(self.embed(src, self.src_lut), src_mask, fault=enc_fault)
         ys = np.full((B, 1), start, np.int64)
-        if not kv_cache:
-            for _ in range(max_len - 1):
+        if not kv_cache or dec_fault is not None:
+            # a decoder fault corrupts the decoder run of step fault_step only
+            # (parallelized_inject_onnx_transformer.py:639: target_inference_number - 1)
+            for i in range(max_len - 1):
                 T = ys.shape[1]
                 out = self.decode(self.embed(ys, self.tgt_lut), memory, src_mask,
-                                  np.tril(np.ones((1, T, T), np.int64)))
+                                  np.tril(np.ones((1, T, T), np.int64)),
+                                  fault=dec_fault if i == fault_step else None)
                 _, nxt = self.generator(out[:, -1])
                 ys = np.concatenate([ys, nxt[:, None]], axis=1)
             return ys

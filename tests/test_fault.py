@@ -282,3 +282,25 @@ def test_oracle_attention_fault_semantics():
     got, _ = O.attention(q, sq, k, sk, v, sv, mask, fault=dict(
         kind="PV_WEIGHT", b=0, h=2, i=0, j=5, d=7, lo=0, hi=S, bit=6, value=0.0))
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,linear,step", [("INPUT", "FFN1", 1), ("WEIGHT", "CPV", 3),
+                                              ("RANDOM", "QK", 2)])
+def test_greedy_decode_with_decoder_fault(torch_gpu, gpu_model, oracle_model, kind, linear, step):
+    """The reference campaign's decode loop with a decoder fault at one step
+    (target_inference_number), full-prefix recompute per step, == the oracle."""
+    from qtx.decode import greedy_decode_fault
+    B, S, L = 2, 14, 8
+    src, m, _ = _enc_inputs(oracle_model, B, S, 31)
+    rng = np.random.default_rng(9)
+    T = step                                       # prefix length of the faulty step
+    if linear in F.ATTN:
+        f = F.random_attn_fault(rng, kind, 1, 3, linear, B, T, S if linear[0] == "C" else T, bit=7)
+    else:
+        f = F.random_fault(rng, kind, 1, 3, linear, B * T, bit=7)
+    if kind == "RANDOM":
+        f.value = 1e4
+    ys = greedy_decode_fault(gpu_model, src, m, L, 0, fault=f, target_inference_number=step)
+    ref = oracle_model.greedy_decode(src, m, max_len=L, fault=f.as_dict(), fault_step=step - 1)
+    np.testing.assert_array_equal(ys, ref)
