@@ -102,6 +102,9 @@ struct qtx_model {
   hipStream_t gstream[QTX_MAX_GROUPS] = {};
   hipEvent_t ev_in = nullptr, ev_out[QTX_MAX_GROUPS] = {};
   std::map<GraphKey, std::vector<hipGraphExec_t>> graphs;   // one graph per sub-batch
+  // encoder sub-batch pipelining: second stream + fork/lag/join events (lazily created)
+  hipStream_t estream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_lag = nullptr, ev_join = nullptr;
   void clear_graphs() {
     for (auto& kv : graphs)
       for (hipGraphExec_t e : kv.second) (void)hipGraphExecDestroy(e);
@@ -297,6 +300,9 @@ int32_t qtx_model_destroy(qtx_model* m) {
     if (s) (void)hipStreamSynchronize(s);
   m->clear_graphs();
   if (m->ev_in) (void)hipEventDestroy(m->ev_in);
+  for (hipEvent_t e : {m->ev_fork, m->ev_lag, m->ev_join})
+    if (e) (void)hipEventDestroy(e);
+  if (m->estream) (void)hipStreamDestroy(m->estream);
   for (int i = 0; i < QTX_MAX_GROUPS; ++i) {
     if (m->ev_out[i]) (void)hipEventDestroy(m->ev_out[i]);
     if (m->gstream[i]) (void)hipStreamDestroy(m->gstream[i]);
@@ -629,7 +635,8 @@ int check_fault(const qtx_model* m, const qtx_fault* f, int module, long B, long
 }
 
 int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, int S,
-                float* out, Scratch& s, hipStream_t st, const qtx_fault* f = nullptr) {
+                float* out, Scratch& s, hipStream_t st, const qtx_fault* f = nullptr,
+                hipEvent_t after_first = nullptr) {
   const qtx_config& c = m->cfg;
   const int D = c.d_model, M = B * S;
   if (x != s.x) HIPCHK(hipMemcpyAsync(s.x, x, (size_t)M * D * 4, hipMemcpyDeviceToDevice, st));
@@ -650,6 +657,7 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
     const EncLayer& L = m->enc[l];
     auto fa = [&](GemmId gid) { return fault_for(f, 0, l, gid, M, c); };
     RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st, fa(G_QKV)));
+    if (l == 0 && after_first) HIPCHK(hipEventRecord(after_first, st));
     AttnArgs a = attn_args(s, B, S, S, S);
     a.mask = mask; a.m_bs = S; a.m_is = 0;
     a.c_ld = D;
@@ -676,9 +684,21 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
   return QTX_OK;
 }
 
+// Encoder sub-batch pipelining: a batch of >= 256 sentences runs as two halves on two
+// streams, the second half one kernel behind, so the HBM-bound epilogues (residual +
+// LayerNorm) of one half overlap the MFMA / VALU-bound kernels (attention, FFN) of the
+// other on different CUs.  Results are identical (rows are independent).
+bool enc_split(int B) { return B >= 256 && !getenv("QTX_ENC_NOSPLIT"); }
+
 size_t enc_ws(const qtx_config& c, int B, int S) {
   Arena ar;
   carve_scratch(ar, c, (long)B * S);
+  if (enc_split(B)) {
+    Arena a2;
+    carve_scratch(a2, c, (long)(B / 2) * S);
+    carve_scratch(a2, c, (long)(B - B / 2) * S);
+    ar.used = std::max(ar.used, a2.used);
+  }
   return align_up(ar.used);
 }
 
@@ -1012,8 +1032,35 @@ int32_t qtx_encoder_forward_fault(const qtx_model* m, const float* x, const uint
   RC(check_fault(m, f, 0, B, S, 0));
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
-  Scratch s = carve_scratch(ar, m->cfg, (long)B * S);
-  return encoder_run(m, x, src_mask, B, S, out, s, (hipStream_t)stream, f);
+  hipStream_t st = (hipStream_t)stream;
+  if (!enc_split(B) || (f && f->kind != QTX_FAULT_NONE)) {
+    Scratch s = carve_scratch(ar, m->cfg, (long)B * S);
+    return encoder_run(m, x, src_mask, B, S, out, s, st, f);
+  }
+  qtx_model* mm = const_cast<qtx_model*>(m);
+  {
+    std::lock_guard<std::mutex> lk(mm->mu);
+    if (!mm->estream) {
+      HIPCHK(hipStreamCreateWithFlags(&mm->estream, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&mm->ev_fork, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&mm->ev_lag, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&mm->ev_join, hipEventDisableTiming));
+    }
+  }
+  const int B0 = B / 2, B1 = B - B0;
+  const long D = m->cfg.d_model;
+  Scratch s0 = carve_scratch(ar, m->cfg, (long)B0 * S);
+  Scratch s1 = carve_scratch(ar, m->cfg, (long)B1 * S);
+  // half 1 starts when half 0's first layer has passed its QKV GEMM (ev_lag)
+  HIPCHK(hipEventRecord(mm->ev_fork, st));
+  HIPCHK(hipStreamWaitEvent(mm->estream, mm->ev_fork, 0));
+  RC(encoder_run(m, x, src_mask, B0, S, out, s0, st, nullptr, mm->ev_lag));
+  HIPCHK(hipStreamWaitEvent(mm->estream, mm->ev_lag, 0));
+  RC(encoder_run(m, x + (long)B0 * S * D, src_mask + (long)B0 * S, B1, S, out + (long)B0 * S * D,
+                 s1, mm->estream, nullptr));
+  HIPCHK(hipEventRecord(mm->ev_join, mm->estream));
+  HIPCHK(hipStreamWaitEvent(st, mm->ev_join, 0));
+  return QTX_OK;
 }
 
 int32_t qtx_encoder_forward(const qtx_model* m, const float* x, const uint8_t* src_mask,

@@ -205,8 +205,14 @@ __device__ __forceinline__ int r_slot(int r, int c) { return c ^ ((r >> 1) & 7);
 
 // FULL: every row of every tile is < M (M % 128 == 0): the epilogue stores carry no row
 // guards, so no divergent branch sits between a load and its use (the compiler's counted
-// vmcnt waits would otherwise fall back to waiting for every store in flight)
-template <int EPI, bool FULL>
+// vmcnt waits would otherwise fall back to waiting for every store in flight).
+// FAULT: the fault-injection variant (RowGemmArgs::fault); the product kernels carry none
+// of its code or registers.
+// Measured and not kept: a persistent variant (grid = #CUs, next tile's first K step
+// prefetched under the epilogue) and software-pipelined fragment reads: within noise —
+// the main loop is bound by the L2 -> LDS fill (~75 GB/s per CU), not by LDS latency or
+// workgroup turnover.
+template <int EPI, bool FULL, bool FAULT>
 __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
   __shared__ __attribute__((aligned(16))) uint8_t st0[R_STAGE];
   __shared__ __attribute__((aligned(16))) uint8_t st1[R_STAGE];
@@ -299,7 +305,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
   }
   __syncthreads();                                 // all fragment reads done: LDS reusable
   QTX_STAMP(1);
-  if (g.fault.kind == FK_INPUT || g.fault.kind == FK_WEIGHT) {
+  if (FAULT && (g.fault.kind == FK_INPUT || g.fault.kind == FK_WEIGHT)) {
     // exact integer correction of the accumulators for one bit-flipped int8 operand
     // (the perturbation the reference propagates through the MatMul, inject_utils/layers.py)
     const FaultArgs& f = g.fault;
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
           y[i][j][e] = (EPI == RE_RELU_PMAX || EPI == RE_RELU_QUANT_PMAX) ? (v > 0.0f ? v : 0.0f) : v;
         }
       }
-    if (g.fault.kind == FK_OUTPUT) {   // RANDOM fault models: one MatMul output value replaced
+    if (FAULT && g.fault.kind == FK_OUTPUT) {   // RANDOM fault models: one MatMul output value replaced
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -567,9 +573,10 @@ hipError_t launch_gemm_row(const RowGemmArgs& g, hipStream_t st) {
   if (g.epi == RE_RES_LN && g.N != R_BN) return hipErrorInvalidValue;
   const dim3 grid((g.N / R_BN) * ((g.M + R_BM - 1) / R_BM)), block(512);
   const bool full = g.M % R_BM == 0;
-#define QTX_ROW_LAUNCH(E)                                                           \
-  (full ? (k_gemm_row<E, true><<<grid, block, 0, st>>>(g), 0)                       \
-        : (k_gemm_row<E, false><<<grid, block, 0, st>>>(g), 0))
+#define QTX_ROW_LAUNCH(E)                                                               \
+  (g.fault.kind != FK_NONE ? (k_gemm_row<E, false, true><<<grid, block, 0, st>>>(g), 0)   \
+   : full ? (k_gemm_row<E, true, false><<<grid, block, 0, st>>>(g), 0)                    \
+          : (k_gemm_row<E, false, false><<<grid, block, 0, st>>>(g), 0))
   switch (g.epi) {
     case RE_QUANT: QTX_ROW_LAUNCH(RE_QUANT); break;
     case RE_RES_LN: QTX_ROW_LAUNCH(RE_RES_LN); break;

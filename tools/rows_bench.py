@@ -15,7 +15,7 @@ PEAK = 256 * 4096 * 2 * 2.4e9
 M = 256 * 128
 L = _lib.lib(build=not os.environ.get("QTX_LIB_PATH"))
 stamps = None
-if os.environ.get("QTX_LIB_PATH"):
+if os.environ.get("QTX_LIB_PATH") and "stamps" in os.environ["QTX_LIB_PATH"]:
     stamps = torch.zeros((4096, 16), dtype=torch.int64, device="cuda")
     C.CDLL(os.environ["QTX_LIB_PATH"]).qtx_debug_set_stamps_gemm(C.c_void_p(stamps.data_ptr()))
 rng = np.random.default_rng(0)
