@@ -115,6 +115,69 @@ def pmc_traffic():
         return json.load(f).get("traffic_bytes_per_launch")
 
 
+def time_row_gemms(M=256 * 128, reps=10):
+    """The five QuantLinear launches of one cfg3 encoder layer through qtx_linear_rows on
+    synthetic int8 operands (QKV + per-token quant, O + residual + LN + quant, FFN1 row-max
+    pass, FFN1 ReLU + quant pass, FFN2 + residual + LN + quant): (us per launch, ops)."""
+    import ctypes as C
+
+    import torch
+
+    from qtx import _lib
+    L = _lib.lib(build=False)
+    rng = np.random.default_rng(0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    a512 = T(rng.integers(-127, 128, (M, D)).astype(np.int8))
+    a2048 = T(rng.integers(-127, 128, (M, F)).astype(np.int8))
+    sa = torch.full((M,), 0.01, device="cuda")
+    W = {nk: T(rng.integers(-127, 128, nk).astype(np.int8)) for nk in [(3 * D, D), (D, D), (F, D), (D, F)]}
+    sw = torch.full((F,), 0.01, device="cuda")
+    bias = torch.zeros(F, device="cuda")
+    out8 = torch.empty((M * F,), dtype=torch.int8, device="cuda")
+    os_ = torch.empty((4 * M,), device="cuda")
+    x = torch.randn((M, D), device="cuda")
+    lna, lnb = torch.ones(D, device="cuda"), torch.zeros(D, device="cuda")
+    pm = torch.full((4, M), 3.0, device="cuda")
+    cases = [("qkv_quant", 3 * D, D, a512, dict(epi=0, out8=out8, ldo8=D, o8_ts=M * D, os=os_, os_ts=M)),
+             ("o_res_ln", D, D, a512, dict(epi=1, res=x, xout=x, ln_a=lna, ln_b=lnb, lnq=out8, lns=os_)),
+             ("ffn1_rowmax", F, D, a512, dict(epi=2, pmax_out=pm)),
+             ("ffn1_quant", F, D, a512, dict(epi=3, pmax_in=pm, pmax_n=4, out8=out8, ldo8=F, os=os_)),
+             ("ffn2_res_ln", D, F, a2048, dict(epi=1, res=x, xout=x, ln_a=lna, ln_b=lnb, lnq=out8, lns=os_))]
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    res = {}
+    for name, N, K, a, kw in cases:
+        args = _lib.RowGemm()
+        for k, v in dict(A=a, sa=sa, W=W[(N, K)], sw=sw, bias=bias, M=M, N=N, K=K, **kw).items():
+            setattr(args, k, v.data_ptr() if hasattr(v, "data_ptr") else v)
+        for _ in range(3):
+            _lib.call("qtx_linear_rows", C.byref(args), st)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            L.qtx_linear_rows(C.byref(args), st)
+        e1.record()
+        torch.cuda.synchronize()
+        res[name] = (e0.elapsed_time(e1) / reps * 1e3, 2 * M * N * K)
+    return res
+
+
+def time_decode(model, B, S, L, steps=3, seed=1000):
+    """ms per greedy decode (encoder + L-1 steps) of B synthetic sentences."""
+    import torch
+    src, _ = make_src(np.random.default_rng(seed), B, S)
+    srcd = torch.from_numpy(src).cuda()
+    maskd = (srcd != 2).to(torch.uint8)
+    ids = torch.empty((B, L), dtype=torch.int64, device="cuda")
+    for _ in range(2):
+        model.greedy(srcd, maskd, max_len=L, start=0, out=ids)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        model.greedy(srcd, maskd, max_len=L, start=0, out=ids)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
 def cpu_baseline(sd, B=4, S=72, max_len=72, seed=7):
     """Numpy oracle greedy decode (KV cached) on a bounded sample, on this host's cores."""
     from oracle.qtx_oracle import OracleModel
@@ -230,10 +293,25 @@ def main():
             torch.cuda.synchronize()
             te = e0.elapsed_time(e1) / 1e3 / n
             ops = encoder_gemm_ops(Bc, Sc)
-            out["cfg3_encoder"] = {"B": Bc, "S": Sc, "ms": te * 1e3,
-                                   "quantlinear_int8_ops": ops,
-                                   "whole_encoder_ops_per_s": ops / te,
-                                   "frac_of_int8_peak_whole_encoder": ops / te / PEAK_INT8_OPS}
+            g = time_row_gemms(Bc * Sc)
+            gemm_us = sum(t for t, _ in g.values())
+            gemm_ops = sum(o for name, (_, o) in g.items() if name != "ffn1_rowmax")
+            out["cfg3_encoder"] = {
+                "B": Bc, "S": Sc, "ms": te * 1e3, "quantlinear_int8_ops": ops,
+                "whole_encoder_ops_per_s": ops / te,
+                "frac_of_int8_peak_whole_encoder": ops / te / PEAK_INT8_OPS,
+                # the layer's QuantLinear launches alone (algorithmic ops: FFN1 counted once
+                # although its per-token output quantization needs two passes)
+                "gemm_us_per_layer": {k: round(t, 1) for k, (t, _) in g.items()},
+                "frac_of_int8_peak_quantlinear_gemms": gemm_ops / (gemm_us * 1e-6) / PEAK_INT8_OPS}
+            # BASELINE configs 4 and 5 (secondary lines): int4 weights at B=32, and the
+            # per-GPU shard of the 8-GPU config (B=2048 / 8 = 256 sentences)
+            m4 = QtxModel(sd, ModelConfig(weight_bits=4))
+            t4 = time_decode(m4, B, S, L)
+            out["cfg4_int4_decode"] = {"B": B, "ms": t4 * 1e3, "tokens_per_s": B * (L - 1) / t4}
+            del m4
+            t5 = time_decode(model, 256, S, L)
+            out["cfg5_per_gpu_decode"] = {"B": 256, "ms": t5 * 1e3, "tokens_per_s": 256 * (L - 1) / t5}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(sd)
         print(json.dumps(out))
