@@ -433,10 +433,10 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
         uint32_t* orow = reinterpret_cast<uint32_t*>(ctx8 + ((long)b * Sq + row) * a.c_ld) + fr;
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
-          int qv[4];
+          float qv[4];
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) qv[dt] = (int)rintf(quot(ctx[h][dt][e], sc[e], inv[e]));
-          orow[16 * h] = pack4_i8(qv[0], qv[1], qv[2], qv[3]);
+          for (int dt = 0; dt < 4; ++dt) qv[dt] = rint_biased(quot(ctx[h][dt][e], sc[e], inv[e]));
+          orow[16 * h] = pack4_biased(qv[0], qv[1], qv[2], qv[3]);
         }
         if (fr == 0) sctx[(long)b * Sq + row] = sc[e];
       }

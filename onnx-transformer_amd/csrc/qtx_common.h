@@ -167,6 +167,17 @@ __device__ __forceinline__ uint32_t pack4_i8(int a, int b, int c, int d) {
          ((uint32_t)(d & 0xff) << 24);
 }
 
+// rint(q) packed as int8 for |q| <= 2^22: RN(q + 1.5 * 2^23) is 1.5 * 2^23 + rint(q)
+// (the add rounds to an integer, ties to even, exactly as rintf: 1.5 * 2^23 is even), so
+// the low byte of its bit pattern is rint(q) in two's complement.  One add per value plus
+// three byte permutes per 4 values, instead of rint + cvt + mask/shift/or.
+__device__ __forceinline__ float rint_biased(float q) { return q + 12582912.0f; }
+__device__ __forceinline__ uint32_t pack4_biased(float t0, float t1, float t2, float t3) {
+  const uint32_t p01 = __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x0c0c0400u);
+  const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(t3), __float_as_uint(t2), 0x0c0c0400u);
+  return __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+}
+
 // rint(x / s) with the correctly rounded quotient, computed as x * (1/s) except within
 // 2^-13 of a rounding tie, where the true division is taken.  Exact: |x/s| <= ~127, so
 // the reciprocal product is within 2^-16 of x/s and fl(x/s) within 2^-18; away from a
@@ -190,8 +201,8 @@ __device__ __forceinline__ void quant_pack(const float* x, float s, uint32_t* ou
   }
 #pragma unroll
   for (int i = 0; i < N / 4; ++i)
-    out[i] = pack4_i8((int)rintf(r[4 * i]), (int)rintf(r[4 * i + 1]), (int)rintf(r[4 * i + 2]),
-                      (int)rintf(r[4 * i + 3]));
+    out[i] = pack4_biased(rint_biased(r[4 * i]), rint_biased(r[4 * i + 1]),
+                          rint_biased(r[4 * i + 2]), rint_biased(r[4 * i + 3]));
 }
 // single value per lane
 __device__ __forceinline__ int quant_one(float x, float s) {

@@ -539,12 +539,12 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int row = m0 + wm * 64 + i * 16 + 4 * fg + e;
-          int qv[8];
+          float qv[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) qv[j] = (int)rintf(quot(yv(i, j, e), sc[i][e], inv[i][e]));
+          for (int j = 0; j < 8; ++j) qv[j] = rint_biased(quot(yv(i, j, e), sc[i][e], inv[i][e]));
           if (FULL || row < g.M)          // the lane's 8 consecutive columns: one 8-byte store
             *reinterpret_cast<uint2*>(ob + (long)row * g.ldo8 + cl) =
-                make_uint2(pack4_i8(qv[0], qv[1], qv[2], qv[3]), pack4_i8(qv[4], qv[5], qv[6], qv[7]));
+                make_uint2(pack4_biased(qv[0], qv[1], qv[2], qv[3]), pack4_biased(qv[4], qv[5], qv[6], qv[7]));
         }
     };
     if (__builtin_expect(__ballot(big) != 0ull, 0))

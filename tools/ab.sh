@@ -1,8 +1,8 @@
 #!/bin/bash
-# A/B on one box: rows_bench + enc_bench with the committed-HEAD build (tools/libqtx_old.so)
+# A/B on one box: rows_bench + enc_bench with the committed-HEAD build ($GRAFT_REPO_ROOT/tools/ab_old.so)
 # and the working-tree build, alternated twice.
 for r in 1 2; do
-  for L in tools/libqtx_old.so onnx-transformer_amd/qtx/libqtx.so; do
+  for L in $GRAFT_REPO_ROOT/tools/ab_old.so $GRAFT_REPO_ROOT/onnx-transformer_amd/qtx/libqtx.so; do
     echo "== $L"
     QTX_LIB_PATH=$L timeout -k 10 100 python tools/rows_bench.py 2>&1 | grep -v amdgpu || exit 1
     QTX_LIB_PATH=$L timeout -k 10 100 python tools/enc_bench.py 2>&1 | grep encoder || exit 1

@@ -6,8 +6,9 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
-sys.path.insert(0, "onnx-transformer_amd")
+_R = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+sys.path.insert(0, _R)
+sys.path.insert(0, _R + "/onnx-transformer_amd")
 from qtx import _lib  # noqa: E402
 
 L = _lib.lib(build=False)

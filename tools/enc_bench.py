@@ -3,8 +3,9 @@ import sys
 
 import torch
 
-sys.path.insert(0, ".")
-sys.path.insert(0, "onnx-transformer_amd")
+_R = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+sys.path.insert(0, _R)
+sys.path.insert(0, _R + "/onnx-transformer_amd")
 from qtx.model import QtxModel  # noqa: E402
 from qtx.weights import ModelConfig, synthetic_state_dict  # noqa: E402
 
