@@ -100,8 +100,9 @@ __device__ __forceinline__ int wave_min_i32(int v) {
 }
 
 // ---------------------------------------------------------------- canonical exp
-// qexp(): Cody-Waite reduction + degree-7 Taylor in Horner form, no FMA.  Identical to
-// oracle/qtx_oracle.py:qexp.  x < -80 returns exactly 0.
+// qexp(): Cody-Waite reduction + degree-7 Taylor in Horner form with fma (7 fused steps
+// instead of 14 separate ones).  Identical to oracle/qtx_oracle.py:qexp (its fma32 is the
+// correctly rounded fma).  x < -80 returns exactly 0.
 __device__ __forceinline__ float qexp(float x) {
   // constants are the exact float32 values the oracle uses (hex literals: no
   // double-rounding ambiguity between the two sides)
@@ -110,13 +111,13 @@ __device__ __forceinline__ float qexp(float x) {
   float r = xc - n * 0x1.62e4p-1f;                      // ln2 hi
   r = r - n * 0x1.7f7d1cp-20f;                         // ln2 lo
   float p = 0x1.a01a02p-13f;                           // 1/5040
-  p = p * r + 0x1.6c16c2p-10f;                         // 1/720
-  p = p * r + 0x1.111112p-7f;                          // 1/120
-  p = p * r + 0x1.555556p-5f;                          // 1/24
-  p = p * r + 0x1.555556p-3f;                          // 1/6
-  p = p * r + 0.5f;
-  p = p * r + 1.0f;
-  p = p * r + 1.0f;
+  p = fmaf(p, r, 0x1.6c16c2p-10f);                     // 1/720
+  p = fmaf(p, r, 0x1.111112p-7f);                      // 1/120
+  p = fmaf(p, r, 0x1.555556p-5f);                      // 1/24
+  p = fmaf(p, r, 0x1.555556p-3f);                      // 1/6
+  p = fmaf(p, r, 0.5f);
+  p = fmaf(p, r, 1.0f);
+  p = fmaf(p, r, 1.0f);
   const float e = ldexpf(p, (int)n);
   return x < -80.0f ? 0.0f : e;
 }

@@ -19,9 +19,9 @@ Parity pinning: tests/test_oracle_golden.py checks this oracle against golden ve
 produced by importing the reference's own PyTorch modules (tests/golden/make_golden.py);
 the ORT CPU path itself is unrunnable here, so ORT-level parity is unpinned.
 
-The fma emulation (:func:`fma32`) computes in float64 and rounds once to float32; it is
-exact except when the float64 rounding lands exactly on a float32 midpoint (probability
-~2^-29 per operation), which is documented in DESIGN.md.
+The fma emulation (:func:`fma32`) is exact: float64 product and sum, with the
+double-rounding case (the float64 sum exactly on a float32 midpoint) corrected from the
+TwoSum error term.
 """
 from __future__ import annotations
 
@@ -39,9 +39,25 @@ EXP_FLUSH = f32(-80.0)         # qexp() returns exactly 0 below this (keeps resu
 # ---------------------------------------------------------------------------------------
 
 def fma32(a, b, c):
-    """float32 fused multiply-add, emulated in float64 (see module docstring)."""
-    return (np.asarray(a, np.float64) * np.asarray(b, np.float64)
-            + np.asarray(c, np.float64)).astype(f32)
+    """Correctly rounded float32 fused multiply-add RN32(a*b + c), exact.
+
+    a*b of two float32 is exact in float64; s = RN64(a*b + c) with the exact error e from
+    TwoSum (a*b + c == s + e).  RN32(s) equals RN32(a*b + c) unless s is exactly a float32
+    midpoint and e != 0 (double rounding): then the result is the neighbour on e's side."""
+    p = np.asarray(a, np.float64) * np.asarray(b, np.float64)
+    c = np.asarray(c, np.float64)
+    s = p + c
+    bb = s - p
+    e = (p - (s - bb)) + (c - bb)
+    r = s.astype(f32)
+    d = s - r.astype(np.float64)
+    up = np.nextafter(r, f32(np.inf)).astype(np.float64) - r.astype(np.float64)
+    dn = r.astype(np.float64) - np.nextafter(r, f32(-np.inf)).astype(np.float64)
+    mid = (d != 0) & (2 * np.abs(d) == np.where(d > 0, up, dn))
+    fix = mid & (e * d > 0)
+    if np.any(fix):
+        r = np.where(fix, np.nextafter(r, np.where(d > 0, f32(np.inf), f32(-np.inf))), r)
+    return np.asarray(r, f32)
 
 
 _H = lambda h: f32(float.fromhex(h))    # exact float32 constants, shared with qtx_common.h
@@ -53,7 +69,7 @@ _LN2_LO = _H("0x1.7f7d1cp-20")
 
 
 def qexp(x):
-    """Canonical fp32 exp: Cody-Waite reduction + degree-7 Taylor, Horner, no FMA.
+    """Canonical fp32 exp: Cody-Waite reduction + degree-7 Taylor, Horner in fma.
 
     Mirrored exactly by ``qexp`` in onnx-transformer_amd/csrc/qtx_common.h.
     Inputs below -80 give exactly 0 (the softmax/log-softmax callers only need e^x for
@@ -64,9 +80,9 @@ def qexp(x):
     n = np.rint(xc * _LOG2E).astype(f32)
     r = xc - n * _LN2_HI
     r = r - n * _LN2_LO
-    p = _EXP_C[0]
+    p = np.full(r.shape, _EXP_C[0], f32)
     for c in _EXP_C[1:]:
-        p = p * r + c
+        p = fma32(p, r, c)
     out = np.ldexp(p.astype(f32), n.astype(np.int32)).astype(f32)
     return np.where(x < EXP_FLUSH, f32(0.0), out).astype(f32)
 
@@ -264,11 +280,10 @@ def attention_pv(qp, qv, sv):
     P = qp.astype(f32) / f32(127.0)                                 # [B,H,Sq,Sk]
     V = qv.astype(f32) * np.asarray(sv, f32)[:, None, :, None]      # [B,H,Sk,dk]
     B, H, Sq, Sk = P.shape
-    acc = np.zeros((B, H, Sq, V.shape[-1]), np.float64)
+    acc = np.zeros((B, H, Sq, V.shape[-1]), f32)
     for j in range(Sk):
-        acc = (P[..., j, None].astype(np.float64) * V[:, :, j, None, :].astype(np.float64)
-               + acc).astype(f32).astype(np.float64)
-    return acc.astype(f32)
+        acc = fma32(P[..., j, None], V[:, :, j, None, :], acc)
+    return acc
 
 
 def split_heads(q, H):
