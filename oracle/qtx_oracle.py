@@ -43,20 +43,21 @@ def fma32(a, b, c):
 
     a*b of two float32 is exact in float64; s = RN64(a*b + c) with the exact error e from
     TwoSum (a*b + c == s + e).  RN32(s) equals RN32(a*b + c) unless s is exactly a float32
-    midpoint and e != 0 (double rounding): then the result is the neighbour on e's side."""
+    midpoint (the 29 mantissa bits below float32 precision read 1000...0) and e != 0
+    (double rounding): then the result is the neighbour on e's side.  (Normal float32
+    results; the callers' values are never subnormal.)"""
     p = np.asarray(a, np.float64) * np.asarray(b, np.float64)
     c = np.asarray(c, np.float64)
     s = p + c
-    bb = s - p
-    e = (p - (s - bb)) + (c - bb)
     r = s.astype(f32)
-    d = s - r.astype(np.float64)
-    up = np.nextafter(r, f32(np.inf)).astype(np.float64) - r.astype(np.float64)
-    dn = r.astype(np.float64) - np.nextafter(r, f32(-np.inf)).astype(np.float64)
-    mid = (d != 0) & (2 * np.abs(d) == np.where(d > 0, up, dn))
-    fix = mid & (e * d > 0)
-    if np.any(fix):
-        r = np.where(fix, np.nextafter(r, np.where(d > 0, f32(np.inf), f32(-np.inf))), r)
+    mid = (np.asarray(s).view(np.int64) & 0x1FFFFFFF) == 0x10000000
+    if np.any(mid):
+        bb = s - p
+        e = (p - (s - bb)) + (c - bb)
+        d = s - r.astype(np.float64)
+        fix = mid & (e * d > 0)
+        if np.any(fix):
+            r = np.where(fix, np.nextafter(r, np.where(d > 0, f32(np.inf), f32(-np.inf))), r)
     return np.asarray(r, f32)
 
 
