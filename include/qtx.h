@@ -227,8 +227,16 @@ typedef struct qtx_row_gemm {
   const float* res; float* xout; const float* ln_a; const float* ln_b;
   int8_t* lnq; float* lns; float* lnout;
   float* pmax_out; const float* pmax_in; int32_t pmax_n;
+  /* kp = 1: A [M (+1 if odd), K] and W in the KP layout (row pair p, K chunk c of 64 bytes
+   * = one 128-byte line at ((p * K/64 + c) * 128), rows 2p | 2p+1 at +0 | +64; W packed by
+   * qtx_pack_w_kp); lnq (epi 1) and out8 (epi 3) are then written KP, epi 0's out8 row-major.
+   * K % 256 == 0. */
+  int32_t kp;
 } qtx_row_gemm;
 int32_t qtx_linear_rows(const qtx_row_gemm* args, void* stream);
+/* W int8 [N, K] row-major -> out [N, K] in the KP layout with the per-512-column-tile row
+ * order qtx_linear_rows(kp = 1) reads.  N % 512 == 0, K % 64 == 0. */
+int32_t qtx_pack_w_kp(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* stream);
 
 /* Skinny int8 GEMM for decode (M small): out = epilogue(A . W^T) with the A operand made
  * in the prologue: amode 0 = int8 A [M,K] + sa; 1 = LayerNorm(X [M,512]; ln_a, ln_b) then

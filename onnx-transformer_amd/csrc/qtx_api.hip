@@ -62,6 +62,7 @@ struct QLin {
   float* s = nullptr;
   float* b = nullptr;
   int N = 0, K = 0;
+  int8_t* qkp = nullptr;   // encoder, 8-bit: q in the row GEMM's KP layout (pack_w_kp)
 };
 
 struct EncLayer {
@@ -197,6 +198,9 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     m->enc.resize(NL);
     m->dec.resize(NL);
     for (auto& e : m->enc) { lin(e.qkv, 3 * D, D); lin(e.o, D, D); lin(e.w1, F, D); lin(e.w2, D, F); }
+    if (c.weight_bits == 8)      // KP copies for the encoder's row GEMMs
+      for (auto& e : m->enc)
+        for (QLin* L : {&e.qkv, &e.o, &e.w1, &e.w2}) L->qkp = ar.take<int8_t>((size_t)L->N * L->K);
     for (auto& d : m->dec) {
       lin(d.qkv, 3 * D, D); lin(d.o, D, D); lin(d.cq, D, D); lin(d.ckv, 2 * D, D);
       lin(d.co, D, D); lin(d.w1, F, D); lin(d.w2, D, F);
@@ -256,6 +260,12 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     Q(d.w2, 0, b + 18, D, F);
   }
   if (rc) { qtx_model_destroy(m); return rc; }
+  for (auto& e : m->enc)
+    for (QLin* L : {&e.qkv, &e.o, &e.w1, &e.w2})
+      if (L->qkp && launch_pack_w_kp(L->q, L->N, L->K, L->qkp, st) != hipSuccess) {
+        qtx_model_destroy(m);
+        return fail(QTX_E_HIP, "KP weight pack");
+      }
   // norms: order of weights.py:norm_names — enc L x 2, enc final, dec L x 3, dec final
   const int nb = norm_tensor_base(c);
   const int n_norms = 5 * NL + 2;
@@ -344,13 +354,13 @@ Scratch carve_scratch(Arena& ar, const qtx_config& c, long M) {
   const int Y = 3 * D > F ? 3 * D : F;
   Scratch s;
   s.x = ar.take<float>(M * D);
-  s.a8 = ar.take<int8_t>(M * F);
+  s.a8 = ar.take<int8_t>((M + 1) * F);    // + 1 row: KP row pairs of an odd M
   s.sa = ar.take<float>(M);
   s.y = ar.take<float>(M * Y);
   s.q8 = ar.take<int8_t>(3 * M * D); s.k8 = s.q8 + M * D; s.v8 = s.k8 + M * D;
   s.sq = ar.take<float>(3 * M); s.sk = s.sq + M; s.sv = s.sk + M;
   s.ctx = ar.take<float>(M * D);
-  s.h8 = ar.take<int8_t>(M * F);
+  s.h8 = ar.take<int8_t>((M + 1) * F);
   s.sh = ar.take<float>(M);
   s.pmax = ar.take<float>((F / 512 + 1) * M);
   return s;
@@ -366,9 +376,9 @@ RowArgs rows_quant(const float* x, long ldx, int rows, int D, int8_t* q, float* 
 }
 
 int ln_quant(const float* x, int rows, const float* const* ln, int D, int8_t* q, float* s,
-             hipStream_t st) {
+             hipStream_t st, bool kp = false) {
   RowArgs a = rows_quant(x, D, rows, D, q, s);
-  a.ln_a = ln[0]; a.ln_b = ln[1];
+  a.ln_a = ln[0]; a.ln_b = ln[1]; a.kp = kp;
   HIPCHK(launch_rows(a, st));
   return QTX_OK;
 }
@@ -381,8 +391,11 @@ int ln_out(const float* x, int rows, const float* const* ln, int D, float* y, hi
   return QTX_OK;
 }
 
-int quant(const float* x, long ldx, int rows, int D, int8_t* q, float* s, hipStream_t st) {
-  HIPCHK(launch_rows(rows_quant(x, ldx, rows, D, q, s), st));
+int quant(const float* x, long ldx, int rows, int D, int8_t* q, float* s, hipStream_t st,
+          bool kp = false) {
+  RowArgs a = rows_quant(x, ldx, rows, D, q, s);
+  a.kp = kp;
+  HIPCHK(launch_rows(a, st));
   return QTX_OK;
 }
 
@@ -401,16 +414,19 @@ int linear(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa
 bool row_path(const qtx_config& c) {
   return c.weight_bits == 8 && c.d_ff % 512 == 0 && !getenv("QTX_NO_ROWGEMM");
 }
-RowGemmArgs rowgemm(const QLin& L, const int8_t* a8, const float* sa, int M, int epi) {
+// kp: A (a8) in the KP layout and W from L.qkp; the int8 lnq / FFN-hidden outputs are
+// then written KP as well (RE_QUANT's q8 stays row-major: attention reads it)
+RowGemmArgs rowgemm(const QLin& L, const int8_t* a8, const float* sa, int M, int epi,
+                    bool kp = false) {
   RowGemmArgs g{};
-  g.A = a8; g.lda = L.K; g.sa = sa; g.W = L.q; g.ldw = L.K; g.sw = L.s; g.bias = L.b;
-  g.M = M; g.N = L.N; g.K = L.K; g.epi = epi;
+  g.A = a8; g.lda = L.K; g.sa = sa; g.W = kp ? L.qkp : L.q; g.ldw = L.K; g.sw = L.s; g.bias = L.b;
+  g.M = M; g.N = L.N; g.K = L.K; g.epi = epi; g.kp = kp;
   return g;
 }
 // out = per-token quantized (a8 . W^T) per 512-wide tile into out8 + t*M*512, os + t*M
 int row_quant(const QLin& L, const int8_t* a8, const float* sa, int M, int8_t* out8,
-              float* os, hipStream_t st, const FaultArgs& fa = FaultArgs{}) {
-  RowGemmArgs g = rowgemm(L, a8, sa, M, RE_QUANT);
+              float* os, hipStream_t st, const FaultArgs& fa = FaultArgs{}, bool kp = false) {
+  RowGemmArgs g = rowgemm(L, a8, sa, M, RE_QUANT, kp);
   g.fault = fa;
   g.out8 = out8; g.ldo8 = 512; g.o8_ts = (long)M * 512; g.os = os; g.os_ts = M;
   HIPCHK(launch_gemm_row(g, st));
@@ -419,8 +435,8 @@ int row_quant(const QLin& L, const int8_t* a8, const float* sa, int M, int8_t* o
 // x += a8 . W^T, then LayerNorm(x) (ln) quantized into (lnq, lns) or fp32 into lnout
 int row_res_ln(const QLin& L, const int8_t* a8, const float* sa, int M, float* x,
                const float* const* ln, int8_t* lnq, float* lns, float* lnout, hipStream_t st,
-               const FaultArgs& fa = FaultArgs{}) {
-  RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RES_LN);
+               const FaultArgs& fa = FaultArgs{}, bool kp = false) {
+  RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RES_LN, kp);
   g.fault = fa;
   g.res = x; g.xout = x; g.ln_a = ln[0]; g.ln_b = ln[1];
   g.lnq = lnq; g.lns = lns; g.lnout = lnout;
@@ -431,8 +447,8 @@ int row_res_ln(const QLin& L, const int8_t* a8, const float* sa, int M, float* x
 // maxima, then recompute + quantize: cheaper than the fp32 hidden's round trip)
 int row_ffn1(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa, int M,
              Scratch& s, hipStream_t st,
-             const FaultArgs& fa = FaultArgs{}) {
-  RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RELU_PMAX);
+             const FaultArgs& fa = FaultArgs{}, bool kp = false) {
+  RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RELU_PMAX, kp);
   g.fault = fa;
   g.pmax_out = s.pmax;
   HIPCHK(launch_gemm_row(g, st));
@@ -651,12 +667,17 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
   // Every LayerNorm + per-token quantization after the first is fused into the epilogue of
   // the GEMM that produces the residual it normalizes (O-proj, FFN2); Q/K/V and the FFN
   // hidden are quantized in their GEMM's epilogue; the last FFN2 applies the final norm.
+  // KP: the int8 activations between the kernels (LN output, attention context, FFN
+  // hidden) live in the KP layout the row GEMM's 64-byte-step DMA reads as full lines
+  // (qtx_common.h kp_off); the fault variants keep the row-major layout.
   const int NL = c.n_layers;
-  RC(ln_quant(s.x, M, m->enc[0].ln[0], D, s.a8, s.sa, st));
+  const bool kp = (f == nullptr || f->kind == QTX_FAULT_NONE) && m->enc[0].qkv.qkp &&
+                  !getenv("QTX_NO_KP");
+  RC(ln_quant(s.x, M, m->enc[0].ln[0], D, s.a8, s.sa, st, kp));
   for (int l = 0; l < NL; ++l) {
     const EncLayer& L = m->enc[l];
     auto fa = [&](GemmId gid) { return fault_for(f, 0, l, gid, M, c); };
-    RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st, fa(G_QKV)));
+    RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st, fa(G_QKV), kp));
     if (l == 0 && after_first) HIPCHK(hipEventRecord(after_first, st));
     AttnArgs a = attn_args(s, B, S, S, S);
     a.mask = mask; a.m_bs = S; a.m_is = 0;
@@ -665,21 +686,24 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
     const hipError_t ea = attn_fault_for(f, 0, l, false, S, S, af)
                               ? hipErrorNotSupported
                               : (getenv("QTX_NO_ATTN_ENCQ") ? hipErrorNotSupported
-                                                            : launch_attention_encq(a, s.a8, s.sa, st));
+                                                            : launch_attention_encq(a, s.a8, s.sa, st,
+                                                                                    false, kp));
     if (attn_fault_for(f, 0, l, false, S, S, af)) {
       RC(attention_fault(a, af, M, D, s, st));
     } else if (ea == hipErrorNotSupported) {  // other shapes: fp32 context + quantization
       HIPCHK(launch_attention(a, st));
-      RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
+      RC(quant(s.ctx, D, M, D, s.a8, s.sa, st, kp));
     } else {
       HIPCHK(ea);
     }
-    RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st, fa(G_O)));
-    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1)));
+    RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st, fa(G_O), kp));
+    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1), kp));
     if (l + 1 < NL)
-      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc[l + 1].ln[0], s.a8, s.sa, nullptr, st, fa(G_FFN2)));
+      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc[l + 1].ln[0], s.a8, s.sa, nullptr, st,
+                    fa(G_FFN2), kp));
     else
-      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc_norm, nullptr, nullptr, out, st, fa(G_FFN2)));
+      RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc_norm, nullptr, nullptr, out, st,
+                    fa(G_FFN2), kp));
   }
   return QTX_OK;
 }
@@ -1375,7 +1399,7 @@ int32_t qtx_linear_rows(const qtx_row_gemm* a, void* stream) {
   g.out8 = a->out8; g.ldo8 = a->ldo8; g.o8_ts = a->o8_ts; g.os = a->os; g.os_ts = a->os_ts;
   g.res = a->res; g.xout = a->xout; g.ln_a = a->ln_a; g.ln_b = a->ln_b;
   g.lnq = a->lnq; g.lns = a->lns; g.lnout = a->lnout;
-  g.pmax_out = a->pmax_out; g.pmax_in = a->pmax_in; g.pmax_n = a->pmax_n;
+  g.pmax_out = a->pmax_out; g.pmax_in = a->pmax_in; g.pmax_n = a->pmax_n; g.kp = a->kp;
   const bool ok = (g.epi == RE_QUANT && g.out8 && g.os) ||
                   (g.epi == RE_RES_LN && g.res && g.xout && g.ln_a && g.ln_b &&
                    (g.lnq ? g.lns != nullptr : g.lnout != nullptr)) ||
@@ -1385,6 +1409,14 @@ int32_t qtx_linear_rows(const qtx_row_gemm* a, void* stream) {
   const hipError_t e = launch_gemm_row(g, (hipStream_t)stream);
   if (e == hipErrorInvalidValue)
     return fail(QTX_E_UNSUPPORTED, "rows GEMM: N=%d K=%d epi=%d", g.N, g.K, g.epi);
+  HIPCHK(e);
+  return QTX_OK;
+}
+
+int32_t qtx_pack_w_kp(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* stream) {
+  if (!W || !out) return fail(QTX_E_INVALID, "null argument");
+  const hipError_t e = launch_pack_w_kp(W, N, K, out, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "pack_w_kp N=%d K=%d", N, K);
   HIPCHK(e);
   return QTX_OK;
 }

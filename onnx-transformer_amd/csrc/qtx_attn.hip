@@ -266,7 +266,7 @@ __device__ __forceinline__ void dma16_lds(const void* gsrc, const void* lds_dst)
                : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
 }
 
-__global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, float* sctx) {
+__global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, float* sctx, int kp) {
   __shared__ __attribute__((aligned(16))) uint8_t Ks[AM_MAXK * 512];
   __shared__ __attribute__((aligned(16))) uint8_t Vs[AM_MAXK * 512];
   __shared__ __attribute__((aligned(16))) float sks[AM_MAXK];     // s_k / 8 (0 if masked), staged order
@@ -430,13 +430,18 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
     for (int e = 0; e < 4; ++e) {
       const int row = r0 + 4 * fg + e;
       if (row < Sq) {
-        uint32_t* orow = reinterpret_cast<uint32_t*>(ctx8 + ((long)b * Sq + row) * a.c_ld) + fr;
+        const long grow = (long)b * Sq + row;
+        uint32_t* orow = reinterpret_cast<uint32_t*>(ctx8 + grow * a.c_ld) + fr;
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
           float qv[4];
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) qv[dt] = rint_biased(quot(ctx[h][dt][e], sc[e], inv[e]));
-          orow[16 * h] = pack4_biased(qv[0], qv[1], qv[2], qv[3]);
+          const uint32_t pk = pack4_biased(qv[0], qv[1], qv[2], qv[3]);
+          if (kp)   // the O-projection reads its A operand in the KP layout
+            *reinterpret_cast<uint32_t*>(ctx8 + kp_off(grow, 64 * h + 4 * fr, 512)) = pk;
+          else
+            orow[16 * h] = pk;
         }
         if (fr == 0) sctx[(long)b * Sq + row] = sc[e];
       }
@@ -452,13 +457,14 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
 // Encoder self-attention with the per-token-quantized context (int8 [B,S,512] with row
 // stride a.c_ld, scales [B*S]); H == 8, Sq == Sk <= 128, per-key mask (m_is == 0).
 hipError_t launch_attention_encq(const AttnArgs& a, int8_t* ctx8, float* sctx, hipStream_t st,
-                                 bool force_encq) {
+                                 bool force_encq, bool kp) {
   if (a.sk_dev || a.qpos_dev || a.H != 8 || a.Sk <= 0 || a.Sk > AM_MAXK || a.Sq != a.Sk ||
       (a.mask && a.m_is != 0) || (a.k_ld % 16) || (a.v_ld % 16) || (a.c_ld % 4))
     return hipErrorNotSupported;
   if (a.B < 128 && !force_encq) return hipErrorNotSupported;   // one workgroup per sentence:
   // below ~128 sentences the per-(head, query block) kernel spreads over more CUs
-  k_attn_encq<<<dim3(a.B), dim3(512), 0, st>>>(a, ctx8, sctx);
+  if (kp && a.c_ld != 512) return hipErrorInvalidValue;
+  k_attn_encq<<<dim3(a.B), dim3(512), 0, st>>>(a, ctx8, sctx, kp ? 1 : 0);
   return hipGetLastError();
 }
 

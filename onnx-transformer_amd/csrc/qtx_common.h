@@ -168,6 +168,14 @@ __device__ __forceinline__ uint32_t pack4_i8(int a, int b, int c, int d) {
          ((uint32_t)(d & 0xff) << 24);
 }
 
+// K-panel-paired ("KP") int8 layout of an [R, K] matrix (R even, K % 64 == 0): rows 2p and
+// 2p+1 of one 64-byte K chunk form one 128-byte line, lines ordered (p, chunk).  A DMA
+// piece of 8 lines then fills a 16-row x 64-byte LDS tile with full-line reads, so the
+// row GEMM can run a 4-stage ring of 64-byte K steps (qtx_gemm.hip, k_gemm_row<.., KP>).
+__host__ __device__ __forceinline__ long kp_off(long r, long k, long K) {
+  return (((r >> 1) * (K >> 6) + (k >> 6)) << 7) + ((r & 1) << 6) + (k & 63);
+}
+
 // rint(q) packed as int8 for |q| <= 2^22: RN(q + 1.5 * 2^23) is 1.5 * 2^23 + rint(q)
 // (the add rounds to an integer, ties to even, exactly as rintf: 1.5 * 2^23 is even), so
 // the low byte of its bit pattern is rint(q) in two's complement.  One add per value plus

@@ -212,10 +212,13 @@ __device__ __forceinline__ int r_slot(int r, int c) { return c ^ ((r >> 1) & 7);
 // prefetched under the epilogue) and software-pipelined fragment reads: within noise —
 // the main loop is bound by the L2 -> LDS fill (~75 GB/s per CU), not by LDS latency or
 // workgroup turnover.
-template <int EPI, bool FULL, bool FAULT>
+template <int EPI, bool FULL, bool FAULT, bool KP>
 __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
-  __shared__ __attribute__((aligned(16))) uint8_t st0[R_STAGE];
-  __shared__ __attribute__((aligned(16))) uint8_t st1[R_STAGE];
+  // one 160 KB LDS array: two 80 KB stages of 128-byte K steps (row-major operands) or
+  // four 40 KB stages of 64-byte K steps (KP operands); the epilogues reuse it
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * R_STAGE];
+  uint8_t* const st0 = lds;
+  uint8_t* const st1 = lds + R_STAGE;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 2, wn = wave & 3;
   const int fr = lane & 15, fg = lane >> 4;
@@ -223,8 +226,94 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
   const int T = gridDim.x, hw = blockIdx.x, q8 = T / 8, rr = T % 8, xcd = hw % 8;
   const int logical = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + hw / 8;
   const int m0 = (logical / ncol) * R_BM, t = logical % ncol, n0 = t * R_BN;
-  const int nk = g.K / R_BK;
   QTX_STAMP(0);
+  auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  v4i acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+
+  if constexpr (KP) {
+    // ---- KP main loop: 64-byte K steps, 4 stages (three in flight while one is
+    // multiplied), every DMA piece 8 full 128-byte lines = 16 rows x 64 B.  LDS rows are
+    // 64 B with the conflict-free slot swizzle of k_gemm256 (g_slot).  Wave w moves A row
+    // pairs 8w..8w+7 (1 piece) and W row pairs 32w..32w+31 (4 pieces) per step.
+    constexpr int KB = 64, KA = R_BM * KB, KSTG = (R_BM + R_BN) * KB;   // 8 KB, 40 KB
+    const int nk = g.K / KB;                      // multiple of 4 (launch check)
+    const long lpr = g.K >> 6;                    // 128-byte lines per row pair
+    const int q = lane & 7, pr = lane >> 3;       // line chunk, pair within the piece
+    const int rsub = 2 * pr + (q >> 2), slot = q & 3;   // LDS row within the piece, slot
+    auto src_off = [&](long pair, int r) {        // this lane's source within a K chunk
+      return ((pair * lpr) << 7) + ((q >> 2) << 6) + 16 * g_slot(r, slot);
+    };
+    const int ra = wave * 16 + rsub;              // A LDS row (0..127)
+    const long aoff = src_off((min(m0 + ra, g.M - 1)) >> 1, ra);
+    long woff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rw = wave * 64 + 16 * i + rsub;   // W LDS row (0..511)
+      woff[i] = src_off((n0 + rw) >> 1, rw);
+    }
+    const int krot = (hw >> 3) % nk;
+    auto issue = [&](uint8_t* base, int kt) {
+      // past the last step: re-load the last one (never read) so every step issues
+      // exactly 5 DMAs and the vmcnt counts stay constant
+      int kk = min(kt, nk - 1) + krot;
+      if (kk >= nk) kk -= nk;
+      const long k0 = (long)kk << 7;              // line index offset of K chunk kk
+      dma16(g.A + aoff + k0, base + wave * 16 * KB);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dma16(g.W + woff[i] + k0, base + KA + (wave * 64 + 16 * i) * KB);
+    };
+    auto compute = [&](const uint8_t* As) {
+      const uint8_t* Bs = As + KA;
+      v4i bfr[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = wn * 128 + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const v4i*>(Bs + r * KB + 16 * g_slot(r, fg));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + i * 16 + fr;
+        const v4i afr = *reinterpret_cast<const v4i*>(As + r * KB + 16 * g_slot(r, fg));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, bfr[j], acc[i][j], 0, 0, 0);
+      }
+    };
+    uint8_t* s0 = lds;
+    uint8_t* s1 = lds + KSTG;
+    uint8_t* s2 = lds + 2 * KSTG;
+    uint8_t* s3 = lds + 3 * KSTG;
+    // top of step kt: this wave's DMAs for kt retired (kt+1, kt+2 may still fly: 5 each),
+    // the barrier makes every wave's part visible and frees stage (kt+3) % 4
+    auto step = [&](uint8_t* cur, uint8_t* nxt3, int kt) {
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      issue(nxt3, kt + 3);
+      compute(cur);
+    };
+    issue(s0, 0);
+    issue(s1, 1);
+    issue(s2, 2);
+    for (int kt = 0; kt < nk; kt += 4) {
+      step(s0, s3, kt);
+      step(s1, s0, kt + 1);
+      step(s2, s1, kt + 2);
+      step(s3, s2, kt + 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing re-loads
+  } else {
+  const int nk = g.K / R_BK;
 
   // DMA (asm: untracked by hipcc, counted by hand; see k_gemm256): one wave-instruction
   // fills 8 LDS rows of 128 B, lane l row l/8, slot l%8 (source chunk = slot ^ swizzle).
@@ -243,13 +332,6 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
     const int n = (rho & ~127) + 8 * (rho & 15) + ((rho >> 4) & 7);   // its output column
     wsrc[i] = g.W + (long)(n0 + n) * g.ldw + 16 * r_slot(rho, lslot);
   }
-  auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
-    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
-  };
   // K steps in rotated order (exact int32 sums: any order gives the same accumulators):
   // the workgroups of one XCD start at different K panels, so they do not all request the
   // same W lines (same L2 channels) at the same time
@@ -263,12 +345,6 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) dma16(wsrc[i] + k0, base + R_ASZ + (wave * 64 + i * 8) * R_BK);
   };
-
-  v4i acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = v4i{0, 0, 0, 0};
   auto compute = [&](const uint8_t* As) {
     const uint8_t* Bs = As + R_ASZ;
 #pragma unroll
@@ -302,6 +378,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
   for (int kt = 0; kt < nk; kt += 2) {
     step(st0, st1, kt);
     if (kt + 1 < nk) step(st1, st0, kt + 1);
+  }
   }
   __syncthreads();                                 // all fragment reads done: LDS reusable
   QTX_STAMP(1);
@@ -445,9 +522,15 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
 #pragma unroll
           for (int r4 = 0; r4 < 4; ++r4)
             if (FULL || rowb + r4 < g.M) {
-              uint32_t* qr = reinterpret_cast<uint32_t*>(g.lnq + (long)(rowb + r4) * R_BN);
-              qr[lane] = qd[r4][0];
-              qr[lane + 64] = qd[r4][1];
+              if constexpr (KP) {      // the next GEMM's A operand in the KP layout
+                const long row = rowb + r4;
+                *reinterpret_cast<uint32_t*>(g.lnq + kp_off(row, 4 * lane, R_BN)) = qd[r4][0];
+                *reinterpret_cast<uint32_t*>(g.lnq + kp_off(row, 4 * (lane + 64), R_BN)) = qd[r4][1];
+              } else {
+                uint32_t* qr = reinterpret_cast<uint32_t*>(g.lnq + (long)(rowb + r4) * R_BN);
+                qr[lane] = qd[r4][0];
+                qr[lane + 64] = qd[r4][1];
+              }
               if (lane == 0) g.lns[rowb + r4] = sc[r4];
             }
         } else {
@@ -542,9 +625,14 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
           float qv[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) qv[j] = rint_biased(quot(yv(i, j, e), sc[i][e], inv[i][e]));
-          if (FULL || row < g.M)          // the lane's 8 consecutive columns: one 8-byte store
-            *reinterpret_cast<uint2*>(ob + (long)row * g.ldo8 + cl) =
-                make_uint2(pack4_biased(qv[0], qv[1], qv[2], qv[3]), pack4_biased(qv[4], qv[5], qv[6], qv[7]));
+          const uint2 pk = make_uint2(pack4_biased(qv[0], qv[1], qv[2], qv[3]),
+                                      pack4_biased(qv[4], qv[5], qv[6], qv[7]));
+          if (FULL || row < g.M) {        // the lane's 8 consecutive columns: one 8-byte store
+            if (KP && EPI == RE_RELU_QUANT_PMAX)   // FFN2's A operand in the KP layout
+              *reinterpret_cast<uint2*>(g.out8 + kp_off(row, n0 + cl, g.ldo8)) = pk;
+            else
+              *reinterpret_cast<uint2*>(ob + (long)row * g.ldo8 + cl) = pk;
+          }
         }
     };
     if (__builtin_expect(__ballot(big) != 0ull, 0))
@@ -571,12 +659,15 @@ hipError_t launch_gemm_row(const RowGemmArgs& g, hipStream_t st) {
   if (g.N % R_BN || g.K % R_BK || g.K <= 0 || (g.lda % 16) || (g.ldw % 16))
     return hipErrorInvalidValue;
   if (g.epi == RE_RES_LN && g.N != R_BN) return hipErrorInvalidValue;
+  if (g.kp && (g.fault.kind != FK_NONE || g.K % 256)) return hipErrorInvalidValue;
   const dim3 grid((g.N / R_BN) * ((g.M + R_BM - 1) / R_BM)), block(512);
   const bool full = g.M % R_BM == 0;
-#define QTX_ROW_LAUNCH(E)                                                               \
-  (g.fault.kind != FK_NONE ? (k_gemm_row<E, false, true><<<grid, block, 0, st>>>(g), 0)   \
-   : full ? (k_gemm_row<E, true, false><<<grid, block, 0, st>>>(g), 0)                    \
-          : (k_gemm_row<E, false, false><<<grid, block, 0, st>>>(g), 0))
+#define QTX_ROW_LAUNCH(E)                                                                      \
+  (g.fault.kind != FK_NONE ? (k_gemm_row<E, false, true, false><<<grid, block, 0, st>>>(g), 0)   \
+   : g.kp ? (full ? (k_gemm_row<E, true, false, true><<<grid, block, 0, st>>>(g), 0)             \
+                  : (k_gemm_row<E, false, false, true><<<grid, block, 0, st>>>(g), 0))            \
+   : full ? (k_gemm_row<E, true, false, false><<<grid, block, 0, st>>>(g), 0)                    \
+          : (k_gemm_row<E, false, false, false><<<grid, block, 0, st>>>(g), 0))
   switch (g.epi) {
     case RE_QUANT: QTX_ROW_LAUNCH(RE_QUANT); break;
     case RE_RES_LN: QTX_ROW_LAUNCH(RE_RES_LN); break;
@@ -585,6 +676,27 @@ hipError_t launch_gemm_row(const RowGemmArgs& g, hipStream_t st) {
     default: return hipErrorInvalidValue;
   }
 #undef QTX_ROW_LAUNCH
+  return hipGetLastError();
+}
+
+// W [N, K] row-major -> KP layout with the per-512-tile LDS column order of k_gemm_row:
+// packed row rho of tile t holds W row t*512 + (rho & ~127) + 8 (rho & 15) + ((rho >> 4) & 7).
+// One thread per 16-byte chunk.
+__global__ void k_pack_w_kp(const int8_t* W, int N, int K, int8_t* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;   // chunk index
+  const long nch = (long)N * (K / 16);
+  if (i >= nch) return;
+  const int rho_g = (int)(i / (K / 16)), kc16 = (int)(i % (K / 16));
+  const int t = rho_g / 512, rho = rho_g % 512;
+  const int n = t * 512 + (rho & ~127) + 8 * (rho & 15) + ((rho >> 4) & 7);
+  *reinterpret_cast<uint4*>(out + kp_off(rho_g, 16L * kc16, K)) =
+      *reinterpret_cast<const uint4*>(W + (long)n * K + 16L * kc16);
+}
+
+hipError_t launch_pack_w_kp(const int8_t* W, int N, int K, int8_t* out, hipStream_t st) {
+  if (N % 512 || K % 64) return hipErrorInvalidValue;
+  const long nch = (long)N * (K / 16);
+  k_pack_w_kp<<<dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, st>>>(W, N, K, out);
   return hipGetLastError();
 }
 

@@ -77,6 +77,7 @@ struct RowArgs {
   int rows, D;
   int rpb; long dst_bstride; const int* dst_off_dev; int dst_off;  // KV-cache scatter
   float qmax;
+  int kp;                     // q in the KP layout ([rows, D], qtx_common.h kp_off)
 };
 
 // Attention core (attention.py:23-36) for one (batch, head) per workgroup.
@@ -136,7 +137,14 @@ struct RowGemmArgs {
   int8_t* lnq; float* lns; float* lnout;
   float* pmax_out; const float* pmax_in; int pmax_n;
   FaultArgs fault;                          // kind FK_NONE: no fault (the product path)
+  // kp: A and W in the KP layout (W rows additionally in the per-512-tile LDS column order,
+  // pack_w_kp), and the int8 lnq / RELU_QUANT out8 outputs written KP (RE_QUANT outputs
+  // stay row-major: attention reads them); no fault support
+  int kp;
 };
+// W [N, K] int8 row-major -> KP layout with the row GEMM's column permutation per 512-wide
+// tile (LDS row rho holds column (rho & ~127) + 8 (rho & 15) + ((rho >> 4) & 7))
+hipError_t launch_pack_w_kp(const int8_t* W, int N, int K, int8_t* out, hipStream_t st);
 hipError_t launch_gemm_row(const RowGemmArgs& a, hipStream_t st);
 
 hipError_t launch_gemm(const GemmArgs& a, int wbits, hipStream_t st);
@@ -175,7 +183,7 @@ hipError_t launch_attention_mfma(const AttnArgs& a, hipStream_t st);
 // token -> ctx8 (row stride a.c_ld) + sctx; hipErrorNotSupported unless H == 8,
 // Sq == Sk <= 128 and the mask is per key (m_is == 0), and (unless forced) B >= 128
 hipError_t launch_attention_encq(const AttnArgs& a, int8_t* ctx8, float* sctx, hipStream_t st,
-                                 bool force_encq = false);
+                                 bool force_encq = false, bool kp = false);
 hipError_t launch_fill_col(int64_t* ids, long bs, int B, int64_t val, hipStream_t st);
 
 }  // namespace qtx

@@ -101,8 +101,14 @@ __global__ __launch_bounds__(256) void k_rows(RowArgs a) {
     int8_t* qr = a.q + dst * a.ldq;
     uint32_t qd[NCH];
     quant_pack<4 * NCH>(&v[0][0], sc, qd);
+    if (a.kp) {
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) *reinterpret_cast<uint32_t*>(qr + 4 * (lane + 64 * c)) = qd[c];
+      for (int c = 0; c < NCH; ++c)
+        *reinterpret_cast<uint32_t*>(a.q + kp_off(dst, 4 * (lane + 64 * c), 256 * NCH)) = qd[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) *reinterpret_cast<uint32_t*>(qr + 4 * (lane + 64 * c)) = qd[c];
+    }
     if (lane == 0) a.s[dst] = sc;
   }
 }

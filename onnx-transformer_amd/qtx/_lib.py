@@ -39,7 +39,7 @@ class RowGemm(C.Structure):
                 ("out8", P), ("ldo8", I64), ("o8_ts", I64), ("os", P), ("os_ts", I64),
                 ("res", P), ("xout", P), ("ln_a", P), ("ln_b", P),
                 ("lnq", P), ("lns", P), ("lnout", P),
-                ("pmax_out", P), ("pmax_in", P), ("pmax_n", I32)]
+                ("pmax_out", P), ("pmax_in", P), ("pmax_n", I32), ("kp", I32)]
 
 class Fault(C.Structure):
     """struct qtx_fault (include/qtx.h)."""
@@ -73,6 +73,7 @@ SIGNATURES = {
     "qtx_layernorm_quant": (I32, [P, P, P, I32, I32, P, P, P, P]),
     "qtx_linear_i8": (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, P, P, P]),
     "qtx_linear_rows": (I32, [C.POINTER(RowGemm), P]),
+    "qtx_pack_w_kp": (I32, [P, I32, I32, P, P]),
     "qtx_pack_int4": (I32, [P, I32, I32, P, P]),
     "qtx_attention_i8": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, P]),
     "qtx_attention_i8_quant": (I32, [P, P, P, P, P, P, P, I32, I32, P, P, P]),

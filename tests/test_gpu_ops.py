@@ -290,3 +290,93 @@ def test_linear_rows_ffn1_two_pass(torch, M):
     q, s = O.quant_rows(h)
     np.testing.assert_array_equal(h8.cpu().numpy(), q)
     np.testing.assert_array_equal(sh.cpu().numpy(), s)
+
+
+def _to_kp(a):
+    """[M, K] int8 -> the KP layout (qtx_common.h kp_off): row pair p, 64-byte K chunk c =
+    one 128-byte line (p * K/64 + c), rows 2p | 2p+1 at +0 | +64; odd M padded by a row."""
+    M, K = a.shape
+    if M & 1:
+        a = np.concatenate([a, np.zeros((1, K), a.dtype)])
+    return np.ascontiguousarray(a.reshape(-1, 2, K // 64, 64).transpose(0, 2, 1, 3)).reshape(-1, K)
+
+
+def _from_kp(a, M):
+    K = a.shape[1]
+    return a.reshape(-1, K // 64, 2, 64).transpose(0, 2, 1, 3).reshape(-1, K)[:M]
+
+
+def _kp_w_order(N):
+    """Row order of qtx_pack_w_kp: packed row rho of 512-column tile t holds W row
+    t*512 + (rho & ~127) + 8 (rho & 15) + ((rho >> 4) & 7)."""
+    rho = np.arange(512)
+    r = (rho & ~127) + 8 * (rho & 15) + ((rho >> 4) & 7)
+    return (np.arange(N // 512)[:, None] * 512 + r[None, :]).reshape(-1)
+
+
+@pytest.mark.parametrize("N,K", [(1536, 512), (512, 2048)])
+def test_pack_w_kp(torch, N, K):
+    rng = np.random.default_rng(N + K)
+    w = rng.integers(-127, 128, (N, K)).astype(np.int8)
+    out = torch.empty((N, K), dtype=torch.int8, device="cuda")
+    from qtx._lib import lib
+    assert lib().qtx_pack_w_kp(P(dev(torch, w)), N, K, P(out), S0) == 0
+    np.testing.assert_array_equal(out.cpu().numpy(), _to_kp(w[_kp_w_order(N)]))
+
+
+@pytest.mark.parametrize("M", [300, 7, 256])
+def test_linear_rows_kp(torch, oracle_model, M):
+    """kp = 1 (the encoder's layout): every epilogue bit-exact against the oracle, int8
+    outputs of epi 1 / 3 in the KP layout, epi 0's Q/K/V row-major."""
+    from qtx._lib import lib
+    rng = np.random.default_rng(M + 99)
+
+    def weights(N, K):
+        qw, sw = O.quant_weight((rng.standard_normal((N, K)) * 0.05).astype(f32), 8)
+        wk = torch.empty((N, K), dtype=torch.int8, device="cuda")
+        assert lib().qtx_pack_w_kp(P(dev(torch, qw)), N, K, P(wk), S0) == 0
+        return qw, sw, wk, rng.standard_normal(N).astype(f32)
+
+    qx, sx = O.quant_rows(rng.standard_normal((M, 512)).astype(f32))
+    ax = dev(torch, _to_kp(qx))
+    # epi 0
+    qw, sw, wk, b = weights(1536, 512)
+    out8 = torch.empty((3, M, 512), dtype=torch.int8, device="cuda")
+    os_ = torch.empty((3, M), dtype=torch.float32, device="cuda")
+    _rows_call(torch, A=ax, sa=dev(torch, sx), W=wk, sw=dev(torch, sw), bias=dev(torch, b),
+               M=M, N=1536, K=512, epi=0, out8=out8, ldo8=512, o8_ts=M * 512, os=os_,
+               os_ts=M, kp=1)
+    y = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b)
+    for t in range(3):
+        q, s = O.quant_rows(y[:, 512 * t:512 * (t + 1)])
+        np.testing.assert_array_equal(out8[t].cpu().numpy(), q)
+        np.testing.assert_array_equal(os_[t].cpu().numpy(), s)
+    # epi 2 + 3 (FFN1), hidden written KP
+    qw, sw, wk, b = weights(2048, 512)
+    pm = torch.empty((4, M), dtype=torch.float32, device="cuda")
+    base = dict(A=ax, sa=dev(torch, sx), W=wk, sw=dev(torch, sw), bias=dev(torch, b),
+                M=M, N=2048, K=512, kp=1)
+    _rows_call(torch, epi=2, pmax_out=pm, **base)
+    h = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b, relu=True)
+    np.testing.assert_array_equal(pm.cpu().numpy(), h.reshape(M, 4, 512).max(-1).T)
+    h8 = torch.zeros((M + (M & 1), 2048), dtype=torch.int8, device="cuda")
+    sh = torch.empty(M, dtype=torch.float32, device="cuda")
+    _rows_call(torch, epi=3, pmax_in=pm, pmax_n=4, out8=h8, ldo8=2048, os=sh, **base)
+    qh, s = O.quant_rows(h)
+    np.testing.assert_array_equal(_from_kp(h8.cpu().numpy(), M), qh)
+    np.testing.assert_array_equal(sh.cpu().numpy(), s)
+    # epi 1 (FFN2: K = 2048 from the KP hidden), next LayerNorm quantized KP
+    qw, sw, wk, b = weights(512, 2048)
+    res = (rng.standard_normal((M, 512)) * 2).astype(f32)
+    la, lb = oracle_model.dec[1]["ln"][0]
+    xd = dev(torch, res.copy())
+    lnq = torch.zeros((M + (M & 1), 512), dtype=torch.int8, device="cuda")
+    lns = torch.empty(M, dtype=torch.float32, device="cuda")
+    _rows_call(torch, A=h8, sa=sh, W=wk, sw=dev(torch, sw), bias=dev(torch, b), M=M, N=512,
+               K=2048, epi=1, res=xd, xout=xd, ln_a=dev(torch, la), ln_b=dev(torch, lb),
+               lnq=lnq, lns=lns, kp=1)
+    x = res + O.linear_epilogue(O.int_gemm(qh, qw), s, sw, b)
+    np.testing.assert_array_equal(xd.cpu().numpy(), x)
+    q, s2 = O.quant_rows(O.layer_norm(x, la, lb))
+    np.testing.assert_array_equal(_from_kp(lnq.cpu().numpy(), M), q)
+    np.testing.assert_array_equal(lns.cpu().numpy(), s2)

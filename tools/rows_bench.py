@@ -14,6 +14,7 @@ from qtx import _lib  # noqa: E402
 
 PEAK = 256 * 4096 * 2 * 2.4e9
 M = 256 * 128
+KP = int(os.environ.get("QTX_BENCH_KP", "1"))
 L = _lib.lib(build=not os.environ.get("QTX_LIB_PATH"))
 stamps = None
 if os.environ.get("QTX_LIB_PATH") and "stamps" in os.environ["QTX_LIB_PATH"]:
@@ -41,6 +42,10 @@ tot = 0.0
 for name, N, K, a, kw in cases:
     args = _lib.RowGemm()
     base = dict(A=a, sa=sa, W=W[(N, K)], sw=sw, bias=bias, M=M, N=N, K=K, **kw)
+    if KP:     # the encoder's layout (random operands: only the weight order matters)
+        wk = torch.empty_like(W[(N, K)])
+        assert L.qtx_pack_w_kp(C.c_void_p(W[(N, K)].data_ptr()), N, K, C.c_void_p(wk.data_ptr()), None) == 0
+        base.update(W=wk, kp=1)
     for k, v in base.items():
         setattr(args, k, v.data_ptr() if hasattr(v, "data_ptr") else v)
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
