@@ -239,6 +239,23 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+  // the epilogue's per-row / per-column scales and bias, loaded before the main loop (their
+  // latency hides under it instead of opening the epilogue)
+  const int cl = wn * 128 + 8 * fr;              // first of the lane's 8 columns in the tile
+  // (KP full-tile instances only: the others have no registers to spare, they would spill)
+  constexpr bool PF = KP && FULL && !FAULT;
+  float sra[4][4];
+  float4 sw4[2], b4[2];
+  auto epi_loads = [&]() {
+    const float4* sp = reinterpret_cast<const float4*>(g.sw + n0 + cl);
+    const float4* bp = reinterpret_cast<const float4*>(g.bias + n0 + cl);
+    sw4[0] = sp[0]; sw4[1] = sp[1]; b4[0] = bp[0]; b4[1] = bp[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sra[i][e] = g.sa[min(m0 + wm * 64 + i * 16 + 4 * fg + e, g.M - 1)];
+  };
+  if constexpr (PF) epi_loads();
 
   if constexpr (KP) {
     // ---- KP main loop: 64-byte K steps, 4 stages (three in flight while one is
@@ -268,6 +285,9 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
       int kk = min(kt, nk - 1) + krot;
       if (kk >= nk) kk -= nk;
       const long k0 = (long)kk << 7;              // line index offset of K chunk kk
+#ifdef QTX_DIAG_NODMA                             // diagnostic builds only (bound decomposition)
+      return;
+#endif
       dma16(g.A + aoff + k0, base + wave * 16 * KB);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dma16(g.W + woff[i] + k0, base + KA + (wave * 64 + 16 * i) * KB);
@@ -286,7 +306,11 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
         const v4i afr = *reinterpret_cast<const v4i*>(As + r * KB + 16 * g_slot(r, fg));
 #pragma unroll
         for (int j = 0; j < 8; ++j)
+#ifdef QTX_DIAG_NOMFMA
+          asm volatile("" ::"v"(afr), "v"(bfr[j]));
+#else
           acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, bfr[j], acc[i][j], 0, 0, 0);
+#endif
       }
     };
     uint8_t* s0 = lds;
@@ -295,6 +319,36 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
     uint8_t* s3 = lds + 3 * KSTG;
     // top of step kt: this wave's DMAs for kt retired (kt+1, kt+2 may still fly: 5 each),
     // the barrier makes every wave's part visible and frees stage (kt+3) % 4
+#ifdef QTX_KP_INTERLEAVE
+    // the 5 DMA pieces of step kt+3 spread between the MFMA groups of step kt
+    auto step = [&](uint8_t* cur, uint8_t* nxt3, int kt) {
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      int kk = min(kt + 3, nk - 1) + krot;
+      if (kk >= nk) kk -= nk;
+      const long k0 = (long)kk << 7;
+      const uint8_t* Bs = cur + KA;
+      v4i bfr[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = wn * 128 + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const v4i*>(Bs + r * KB + 16 * g_slot(r, fg));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + i * 16 + fr;
+        const v4i afr = *reinterpret_cast<const v4i*>(cur + r * KB + 16 * g_slot(r, fg));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (i == 0) dma16(g.A + aoff + k0, nxt3 + wave * 16 * KB);
+        dma16(g.W + woff[i] + k0, nxt3 + KA + (wave * 64 + 16 * i) * KB);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+#else
     auto step = [&](uint8_t* cur, uint8_t* nxt3, int kt) {
       asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -302,6 +356,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
       issue(nxt3, kt + 3);
       compute(cur);
     };
+#endif
     issue(s0, 0);
     issue(s1, 1);
     issue(s2, 2);
@@ -410,13 +465,11 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
   // ---- y = ((float(acc) * sa[m]) * sw[n]) + b[n] (relu for the FFN1 epilogues), computed
   // once in place of the accumulators; lane: rows 4*fg + e of fragment i, columns cb + j
   // (j < 8) with cb = n0 + wn*128 + 8*fr ------------------------------------------------
-  const int cl = wn * 128 + 8 * fr;              // first of the lane's 8 columns in the tile
   float y[4][8][4];
   {
+    if constexpr (!PF) epi_loads();
     float swc[8], bc[8];
-    const float4* sp = reinterpret_cast<const float4*>(g.sw + n0 + cl);
-    const float4* bp = reinterpret_cast<const float4*>(g.bias + n0 + cl);
-    const float4 s0 = sp[0], s1 = sp[1], b0 = bp[0], b1 = bp[1];
+    const float4 s0 = sw4[0], s1 = sw4[1], b0 = b4[0], b1 = b4[1];
     swc[0] = s0.x; swc[1] = s0.y; swc[2] = s0.z; swc[3] = s0.w;
     swc[4] = s1.x; swc[5] = s1.y; swc[6] = s1.z; swc[7] = s1.w;
     bc[0] = b0.x; bc[1] = b0.y; bc[2] = b0.z; bc[3] = b0.w;
@@ -425,7 +478,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float sr = g.sa[min(m0 + wm * 64 + i * 16 + 4 * fg + e, g.M - 1)];
+        const float sr = sra[i][e];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float v = ((float)acc[i][j][e] * sr) * swc[j] + bc[j];
@@ -616,22 +669,38 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
         big |= !(rmax[i][e] < 0x1p37f);
       }
     int8_t* ob = EPI == RE_QUANT ? g.out8 + (long)t * g.o8_ts : g.out8 + n0;
+    // Stores widened to 16 bytes (the tail is store-issue-bound, not HBM-bound): lanes fr,
+    // fr^1 hold columns 8fr..8fr+7 and the next 8 of the same rows; for each pair of rows
+    // (e, e+1) the even lane sends its row-(e+1) half and receives the odd lane's row-e
+    // half (one DPP lane swap per dword), so the even lane stores row e and the odd lane
+    // row e+1, 16 consecutive bytes each: 8 dwordx4 stores per lane instead of 16 dwordx2.
+    const bool odd = fr & 1;
+    const int cw = wn * 128 + 16 * (fr >> 1);     // the pair's 16 columns in the tile
+    auto swap1 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true); };
     auto store_rows = [&](auto quot) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = m0 + wm * 64 + i * 16 + 4 * fg + e;
-          float qv[8];
+        for (int ep = 0; ep < 4; ep += 2) {
+          uint2 pk[2];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) qv[j] = rint_biased(quot(yv(i, j, e), sc[i][e], inv[i][e]));
-          const uint2 pk = make_uint2(pack4_biased(qv[0], qv[1], qv[2], qv[3]),
-                                      pack4_biased(qv[4], qv[5], qv[6], qv[7]));
-          if (FULL || row < g.M) {        // the lane's 8 consecutive columns: one 8-byte store
+          for (int h = 0; h < 2; ++h) {
+            const int e = ep + h;
+            float qv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qv[j] = rint_biased(quot(yv(i, j, e), sc[i][e], inv[i][e]));
+            pk[h] = make_uint2(pack4_biased(qv[0], qv[1], qv[2], qv[3]),
+                               pack4_biased(qv[4], qv[5], qv[6], qv[7]));
+          }
+          const uint32_t r0 = swap1(odd ? pk[0].x : pk[1].x);
+          const uint32_t r1 = swap1(odd ? pk[0].y : pk[1].y);
+          const uint4 v = odd ? make_uint4(r0, r1, pk[1].x, pk[1].y) : make_uint4(pk[0].x, pk[0].y, r0, r1);
+          const int row = m0 + wm * 64 + i * 16 + 4 * fg + ep + (odd ? 1 : 0);
+          if (FULL || row < g.M) {
             if (KP && EPI == RE_RELU_QUANT_PMAX)   // FFN2's A operand in the KP layout
-              *reinterpret_cast<uint2*>(g.out8 + kp_off(row, n0 + cl, g.ldo8)) = pk;
+              *reinterpret_cast<uint4*>(g.out8 + kp_off(row, n0 + cw, g.ldo8)) = v;
             else
-              *reinterpret_cast<uint2*>(ob + (long)row * g.ldo8 + cl) = pk;
+              *reinterpret_cast<uint4*>(ob + (long)row * g.ldo8 + cw) = v;
           }
         }
     };
