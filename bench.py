@@ -5,14 +5,17 @@
 One "step" = one whole greedy decode of one batch of synthetic sentences: encoder, cross
 K/V, max_len-1 = 71 KV-cached decoder steps, generator + argmax (the fixed loop of
 reference/onnx_reference_inference.py:630, no EOS exit).  Workload at N=1 = BASELINE
-config 2: batch 32 per GPU, source length <= 64 padded to 72.  For N > 1 each rank (one
-process per GPU, torchrun) decodes its own 32-sentence shard with its own weight replica:
-weak scaling, no collective on the data path; RCCL is used only for the
-barrier and the max-over-ranks of the elapsed time.
+config 2: batch 32 per GPU, source length <= 64 padded to 72.  For N > 1 one global batch
+(batch x N sentences, or --global-batch, e.g. 2048 for BASELINE config 5) is partitioned
+by source length over the ranks (one process per GPU, torchrun), each decoding its shard
+with its own weight replica: no collective on the data path; RCCL carries
+the barrier, the max-over-ranks of the elapsed time and, after the timed region, the
+all-gather of the ids that rank 0 checks against a re-decoded sample.
 
 Printed JSON (rank 0) adds:
   roofline     dominant kernel, algorithmic bytes per launch / measured avg duration
-  cpu_baseline the numpy oracle (CPU restatement, "port") on a bounded sample, rank 0 only
+  cpu_baseline oracle/torch_port.py (the reference's fp32 fake-quant arithmetic in torch)
+               on bounded samples on the host cores, rank 0 only
   cfg3_encoder encoder-only B=256 S=128 QuantLinear int8 ops/s vs the MFMA int8 peak
 """
 from __future__ import annotations
@@ -138,6 +141,13 @@ def time_row_gemms(M=256 * 128, reps=10):
     x = torch.randn((M, D), device="cuda")
     lna, lnb = torch.ones(D, device="cuda"), torch.zeros(D, device="cuda")
     pm = torch.full((4, M), 3.0, device="cuda")
+    # the encoder runs the KP instances (csrc/qtx_api.hip encoder_run: kp = 1): weights
+    # packed by qtx_pack_w_kp, A in the KP layout (random bytes: any layout of them is)
+    for (N, K), w in list(W.items()):
+        wk = torch.empty_like(w)
+        _lib.call("qtx_pack_w_kp", C.c_void_p(w.data_ptr()), N, K, C.c_void_p(wk.data_ptr()),
+                  C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        W[(N, K)] = wk
     cases = [("qkv_quant", 3 * D, D, a512, dict(epi=0, out8=out8, ldo8=D, o8_ts=M * D, os=os_, os_ts=M)),
              ("o_res_ln", D, D, a512, dict(epi=1, res=x, xout=x, ln_a=lna, ln_b=lnb, lnq=out8, lns=os_)),
              ("ffn1_rowmax", F, D, a512, dict(epi=2, pmax_out=pm)),
@@ -147,7 +157,7 @@ def time_row_gemms(M=256 * 128, reps=10):
     res = {}
     for name, N, K, a, kw in cases:
         args = _lib.RowGemm()
-        for k, v in dict(A=a, sa=sa, W=W[(N, K)], sw=sw, bias=bias, M=M, N=N, K=K, **kw).items():
+        for k, v in dict(A=a, sa=sa, W=W[(N, K)], sw=sw, bias=bias, M=M, N=N, K=K, kp=1, **kw).items():
             setattr(args, k, v.data_ptr() if hasattr(v, "data_ptr") else v)
         for _ in range(3):
             _lib.call("qtx_linear_rows", C.byref(args), st)
@@ -178,24 +188,49 @@ def time_decode(model, B, S, L, steps=3, seed=1000):
     return (time.perf_counter() - t0) / steps
 
 
-def cpu_baseline(sd, B=4, S=72, max_len=72, seed=7):
-    """Numpy oracle greedy decode (KV cached) on a bounded sample, on this host's cores."""
-    from oracle.qtx_oracle import OracleModel
+def cpu_model():
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        threads = os.cpu_count() or 1
-    om = OracleModel(sd)
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(sd, B=32, S=72, max_len=72, seed=7):
+    """The reference's CPU arithmetic (fp32 fake-quant W8A8, oracle/torch_port.py: torch on
+    the host cores, KV-cached) on bounded samples, rank 0 only: cfg2 (B=32 decode, the
+    headline unit), cfg1 (B=1 decode) and cfg3 (encoder B=256 S=128, int8-op rate)."""
+    import torch
+
+    from oracle.torch_port import TorchPortModel
+    threads = torch.get_num_threads()
+    tp = TorchPortModel(sd)
     src, _ = make_src(np.random.default_rng(seed), B, S)
-    mask = (src != 2)[:, None, :]
+    mask = torch.from_numpy((src != 2)[:, None, :])
+    srct = torch.from_numpy(src)
+    tp.greedy_decode(srct[:2], mask[:2], 4)                     # warm the thread pool
     t0 = time.perf_counter()
-    om.greedy_decode(src, mask, max_len=max_len)
-    dt = time.perf_counter() - t0
-    return {"value": B * (max_len - 1) / dt, "unit": "decoded tokens/s", "cores": int(threads),
+    tp.greedy_decode(srct, mask, max_len)
+    t2 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    tp.greedy_decode(srct[:1], mask[:1], max_len)
+    t1 = time.perf_counter() - t0
+    xe = torch.randn((256, 128, D))
+    me = torch.ones((256, 1, 128), dtype=torch.bool)
+    t0 = time.perf_counter()
+    tp.encode(xe, me)
+    t3 = time.perf_counter() - t0
+    return {"value": B * (max_len - 1) / t2, "unit": "decoded tokens/s", "cores": int(threads),
             "kind": "port",
-            "sample": f"numpy oracle greedy decode, B={B} sentences, S={S}, {max_len - 1} steps, "
-                      f"KV-cached, {dt:.1f}s"}
+            "sample": f"oracle/torch_port.py (the reference's fp32 fake-quant arithmetic in "
+                      f"torch, KV-cached) on {threads} threads of '{cpu_model()}': cfg2 greedy "
+                      f"decode B={B}, S={S}, {max_len - 1} steps in {t2:.1f}s",
+            "cfg1_b1_decode_tokens_per_s": (max_len - 1) / t1,
+            "cfg3_encoder_s": t3,
+            "cfg3_encoder_int8_ops_per_s": encoder_gemm_ops(256, 128) / t3}
 
 
 def main():
@@ -203,7 +238,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=32, help="sentences per GPU")
+    ap.add_argument("--batch", type=int, default=32, help="sentences per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="total sentences over all ranks (cfg5: 2048); default batch x world")
     ap.add_argument("--src-len", type=int, default=72)
     ap.add_argument("--max-len", type=int, default=72)
     ap.add_argument("--weight-bits", type=int, default=8)
@@ -226,15 +263,20 @@ def main():
         _build.build()
     if world > 1:
         dist.barrier()
-    from qtx.decode import greedy_decode
+    from qtx.decode import gather_ids, greedy_decode, length_sorted_shards
     from qtx.model import QtxModel
     from qtx.weights import ModelConfig, synthetic_state_dict
 
     sd = synthetic_state_dict(20241223)
     model = QtxModel(sd, ModelConfig(weight_bits=args.weight_bits))
-    B, S, L = args.batch, args.src_len, args.max_len
-    src, lens = make_src(np.random.default_rng(1000 + rank), B, S)
-    srcd = torch.from_numpy(src).cuda()
+    S, L = args.src_len, args.max_len
+    # one global batch (same seed on every rank), partitioned by source length:
+    # each rank decodes its shard; no collective on the data path
+    G = args.global_batch or args.batch * world
+    gsrc, glens = make_src(np.random.default_rng(20241223), G, S)
+    idx = length_sorted_shards(glens, world)[rank]
+    B = len(idx)
+    srcd = torch.from_numpy(gsrc[idx]).cuda()
     maskd = (srcd != 2).to(torch.uint8)
     ids = torch.empty((B, L), dtype=torch.int64, device="cuda")
 
@@ -257,25 +299,51 @@ def main():
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    tokens = world * B * (L - 1) * args.steps
+    tokens = G * (L - 1) * args.steps
     value = tokens / dt
 
+    # after the timed region: gather every rank's ids into global order and, on rank 0,
+    # re-decode a sample of sentences from every shard in one batch of its own (per-token
+    # quantization: a sentence's tokens do not depend on its batch)
+    allids = gather_ids(dist, ids, idx, G, world) if world > 1 else None
+    verified = None
     if rank == 0:
-        kt = time_dominant(B)
-        alg = dominant_alg_bytes(B)
-        roof = {"kernel": f"{DOMINANT}: LN+QKV decode GEMM (M={B}, N={3 * D}, K={D}, int8)",
+        if allids is None:
+            allids = np.full((G, L), -1, np.int64)
+            allids[idx] = ids.cpu().numpy()
+        shards = length_sorted_shards(glens, world)
+        pick = np.unique(np.concatenate([sh[[0, len(sh) // 2, -1]] for sh in shards if len(sh)]))
+        ref = greedy_decode(model, gsrc[pick], (gsrc[pick] != 2)[:, None, :], L, 0)
+        verified = bool((allids >= 0).all() and np.array_equal(ref, allids[pick]))
+
+    if rank == 0:
+        kt = time_dominant(min(B, 32))
+        alg = dominant_alg_bytes(min(B, 32))
+        roof = {"kernel": f"{DOMINANT}: LN+QKV decode GEMM (M={min(B, 32)}, N={3 * D}, K={D}, int8)",
                 "bound": "hbm", "achieved": alg / kt / 1e9, "peak": PEAK_HBM / 1e9,
                 "unit": "GB/s", "frac": alg / kt / PEAK_HBM, "traffic": pmc_traffic(),
                 "avg_us": kt * 1e6, "alg_bytes_per_launch": alg}
-        out = {"metric": "decoded tokens/sec IWSLT14 de-en int8 greedy (batch 32/GPU, 71 steps)",
+        # the public API path (numpy in, numpy out, fresh buffers each call)
+        pub = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            greedy_decode(model, gsrc[idx], (gsrc[idx] != 2)[:, None, :], L, 0)
+            pub.append(time.perf_counter() - t0)
+        out = {"metric": "decoded tokens/sec IWSLT14 de-en int8 greedy "
+                         f"(batch {G} over {world} GPU, {L - 1} steps)",
                "value": value, "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "higher_is_better": True,
+               "scaling": "weak" if not args.global_batch else "strong",
+               "vs_baseline": None,
                "dtype": "int8" if args.weight_bits == 8 else "int4w-int8a",
                "data": "synthetic (seeded src ids, random-init weights of the reference architecture)",
-               "config": {"workload": f"cfg2: greedy decode B={B}/GPU, src<=64 padded to {S}, "
-                                      f"max_len={L}", "global_batch": B * world, "seq_len": S,
+               "config": {"workload": f"cfg2: greedy decode, src<=64 padded to {S}, max_len={L}, "
+                                      f"{G} sentences length-sorted over {world} rank(s)",
+                          "global_batch": G, "per_gpu_batch": B, "seq_len": S,
                           "parallelism": f"sentence-shard x{world}"},
+               "ids_verified_vs_single_batch_sample": verified,
+               "public_api_ms_per_decode": min(pub) * 1e3,
                "roofline": roof}
         if not args.no_cfg3:
             Bc, Sc = 256, 128
@@ -300,15 +368,15 @@ def main():
                 "B": Bc, "S": Sc, "ms": te * 1e3, "quantlinear_int8_ops": ops,
                 "whole_encoder_ops_per_s": ops / te,
                 "frac_of_int8_peak_whole_encoder": ops / te / PEAK_INT8_OPS,
-                # the layer's QuantLinear launches alone (algorithmic ops: FFN1 counted once
-                # although its per-token output quantization needs two passes)
+                # the layer's QuantLinear launches alone, KP instances (algorithmic ops:
+                # FFN1 counted once although its per-token quantization needs two passes)
                 "gemm_us_per_layer": {k: round(t, 1) for k, (t, _) in g.items()},
                 "frac_of_int8_peak_quantlinear_gemms": gemm_ops / (gemm_us * 1e-6) / PEAK_INT8_OPS}
             # BASELINE configs 4 and 5 (secondary lines): int4 weights at B=32, and the
             # per-GPU shard of the 8-GPU config (B=2048 / 8 = 256 sentences)
             m4 = QtxModel(sd, ModelConfig(weight_bits=4))
-            t4 = time_decode(m4, B, S, L)
-            out["cfg4_int4_decode"] = {"B": B, "ms": t4 * 1e3, "tokens_per_s": B * (L - 1) / t4}
+            t4 = time_decode(m4, 32, S, L)
+            out["cfg4_int4_decode"] = {"B": 32, "ms": t4 * 1e3, "tokens_per_s": 32 * (L - 1) / t4}
             del m4
             t5 = time_decode(model, 256, S, L)
             out["cfg5_per_gpu_decode"] = {"B": 256, "ms": t5 * 1e3, "tokens_per_s": 256 * (L - 1) / t5}

@@ -74,14 +74,20 @@ struct DecLayer {
   const float* ln[3][2];
 };
 
+// The captured decode graphs depend on the shapes and the workspace only: the caller's
+// ids and src_mask are staged through workspace buffers around each replay, so callers
+// that allocate fresh id/mask tensors per call still hit the cache.
 struct GraphKey {
   int B, S, L, G;
-  const void *ws, *ids, *mask;
+  const void* ws;
   std::string variant;   // the QTX_* experiment switches the captured step depends on
   bool operator<(const GraphKey& o) const {
-    return std::tie(B, S, L, G, ws, ids, mask, variant) <
-           std::tie(o.B, o.S, o.L, o.G, o.ws, o.ids, o.mask, o.variant);
+    return std::tie(B, S, L, G, ws, variant) < std::tie(o.B, o.S, o.L, o.G, o.ws, o.variant);
   }
+};
+struct GraphEntry {
+  std::vector<hipGraphExec_t> execs;   // one graph per sub-batch
+  hipEvent_t done = nullptr;           // recorded after the entry's last replay
 };
 
 // The fused decode runs the batch as up to QTX_MAX_GROUPS independent sub-batches, each a
@@ -102,16 +108,38 @@ struct qtx_model {
   std::mutex mu;
   hipStream_t gstream[QTX_MAX_GROUPS] = {};
   hipEvent_t ev_in = nullptr, ev_out[QTX_MAX_GROUPS] = {};
-  std::map<GraphKey, std::vector<hipGraphExec_t>> graphs;   // one graph per sub-batch
+  std::map<GraphKey, GraphEntry> graphs;
   // encoder sub-batch pipelining: second stream + fork/lag/join events (lazily created)
   hipStream_t estream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_lag = nullptr, ev_join = nullptr;
+  int device = 0;            // the device the model's memory lives on
+  // an exec may still be running on a caller's stream: wait for its last replay first
   void clear_graphs() {
-    for (auto& kv : graphs)
-      for (hipGraphExec_t e : kv.second) (void)hipGraphExecDestroy(e);
+    for (auto& kv : graphs) {
+      if (kv.second.done) {
+        (void)hipEventSynchronize(kv.second.done);
+        (void)hipEventDestroy(kv.second.done);
+      }
+      for (hipGraphExec_t e : kv.second.execs) (void)hipGraphExecDestroy(e);
+    }
     graphs.clear();
   }
 };
+
+namespace {
+// Makes the model's device current for the lifetime of the guard (streams and events are
+// created on the current device), restoring the caller's device afterwards.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+    else prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+}  // namespace
 
 namespace {
 
@@ -217,6 +245,7 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
   };
   qtx_model* m = new qtx_model();
   m->cfg = c;
+  (void)hipGetDevice(&m->device);
   Arena sizing;
   carve(m, sizing);
   const size_t bytes = align_up(sizing.used);
@@ -810,6 +839,8 @@ struct GreedyWS {
   // fused-decode sub-batches: step scratch (grp[0] = dec) and step counters, 4 ints each
   std::vector<Scratch> grp;
   int* gsteps;
+  int64_t* ids;       // [B][max_len] the decode writes here; copied out to the caller's ids
+  uint8_t* mask;      // [B][S] staged copy of the caller's src_mask
 };
 
 // Sub-batch split of the fused decode.  Sentences are independent (per-token quantization:
@@ -852,6 +883,8 @@ GreedyWS carve_greedy(Arena& ar, const qtx_config& c, int B, int S, int max_len)
   g.grp.push_back(g.dec);
   for (int i = 1; i < gr.G; ++i) g.grp.push_back(carve_scratch(ar, c, gr.Bg));
   g.gsteps = ar.take<int>(4 * QTX_MAX_GROUPS);
+  g.ids = ar.take<int64_t>((size_t)B * max_len);
+  g.mask = ar.take<uint8_t>((size_t)B * S);
   return g;
 }
 
@@ -1030,6 +1063,9 @@ bool env_flag(const char* name) {
   return v && *v && strcmp(v, "0") != 0;
 }
 
+int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S, int max_len,
+               int64_t start, const qtx_fault* f, hipStream_t st);
+
 }  // namespace
 
 extern "C" {
@@ -1061,15 +1097,17 @@ int32_t qtx_encoder_forward_fault(const qtx_model* m, const float* x, const uint
     Scratch s = carve_scratch(ar, m->cfg, (long)B * S);
     return encoder_run(m, x, src_mask, B, S, out, s, st, f);
   }
+  // The model's second stream and its three events are shared by every caller: the lock
+  // is held across the whole record / wait sequence, so two threads' fork, lag and join
+  // records cannot interleave (a wait always pairs with its own call's record).
   qtx_model* mm = const_cast<qtx_model*>(m);
-  {
-    std::lock_guard<std::mutex> lk(mm->mu);
-    if (!mm->estream) {
-      HIPCHK(hipStreamCreateWithFlags(&mm->estream, hipStreamNonBlocking));
-      HIPCHK(hipEventCreateWithFlags(&mm->ev_fork, hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&mm->ev_lag, hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&mm->ev_join, hipEventDisableTiming));
-    }
+  std::lock_guard<std::mutex> lk(mm->mu);
+  DeviceGuard dg(mm->device);
+  if (!mm->estream) {
+    HIPCHK(hipStreamCreateWithFlags(&mm->estream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&mm->ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&mm->ev_lag, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&mm->ev_join, hipEventDisableTiming));
   }
   const int B0 = B / 2, B1 = B - B0;
   const long D = m->cfg.d_model;
@@ -1218,10 +1256,35 @@ int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
                                    "qtx_decoder_forward_fault on the step's prefix)");
   RC(check_fault(m, f, 0, B, S, 0));
   hipStream_t st = (hipStream_t)stream;
-  const int D = c.d_model;
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
   GreedyWS g = carve_greedy(ar, c, B, S, max_len);
+  // the decode reads the workspace's copy of src_mask and writes the workspace's ids
+  // (the captured graphs then depend on the workspace only); ids go out at the end
+  HIPCHK(hipMemcpyAsync(g.mask, src_mask, (size_t)B * S, hipMemcpyDeviceToDevice, st));
+  RC(greedy_run(m, g, src, B, S, max_len, start, f, st));
+  HIPCHK(hipMemcpyAsync(ids, g.ids, (size_t)B * max_len * sizeof(int64_t),
+                        hipMemcpyDeviceToDevice, st));
+  return QTX_OK;
+}
+
+int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t* src_mask,
+                          int32_t B, int32_t S, int32_t max_len, int64_t start, int64_t* ids,
+                          void* ws, size_t ws_bytes, void* stream) {
+  return qtx_greedy_decode_fault(m, src, src_mask, B, S, max_len, start, ids, ws, ws_bytes,
+                                 nullptr, stream);
+}
+
+}  // extern "C"
+
+namespace {
+
+int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S, int max_len,
+               int64_t start, const qtx_fault* f, hipStream_t st) {
+  const qtx_config& c = m->cfg;
+  const int D = c.d_model;
+  const uint8_t* src_mask = g.mask;
+  int64_t* ids = g.ids;
 
   // encoder: memory = encode(src_embed(src), src_mask)
   HIPCHK(launch_embed(src, S, B, S, nullptr, 0, m->src_lut, c.src_vocab, m->pe, c.max_len,
@@ -1261,6 +1324,7 @@ int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
   // into the caller's stream.
   qtx_model* mm = const_cast<qtx_model*>(m);
   std::lock_guard<std::mutex> lock(mm->mu);
+  DeviceGuard dg(mm->device);
   if (!mm->ev_in) HIPCHK(hipEventCreateWithFlags(&mm->ev_in, hipEventDisableTiming));
   for (int i = 0; i < gr.G; ++i)
     if (!mm->gstream[i]) {
@@ -1278,7 +1342,7 @@ int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
     const char* v = getenv(k);
     variant += std::string(k) + "=" + (v ? v : "") + ";";
   }
-  const GraphKey key{B, S, max_len, gr.G * 1000 + per_graph, ws, ids, src_mask, variant};
+  const GraphKey key{B, S, max_len, gr.G * 1000 + per_graph, g.gsteps, variant};
   auto it = mm->graphs.find(key);
   if (it == mm->graphs.end()) {
     if (mm->graphs.size() >= 16) mm->clear_graphs();
@@ -1305,7 +1369,9 @@ int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
       if (e != hipSuccess) { drop(); HIPCHK(e); }
       execs.push_back(exec);
     }
-    it = mm->graphs.emplace(key, std::move(execs)).first;
+    GraphEntry ent;
+    ent.execs = std::move(execs);
+    it = mm->graphs.emplace(key, std::move(ent)).first;
   }
   // One sub-batch: replay on the caller's stream itself (a graph captured on one stream can
   // be launched on any).  Several: fork to the model's streams and join back.
@@ -1324,7 +1390,7 @@ int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
     HIPCHK(hipEventRecord(tg0, ls[0]));
   }
   for (int t = 0; t < (max_len - 1) / per_graph; ++t)
-    for (int i = 0; i < gr.G; ++i) HIPCHK(hipGraphLaunch(it->second[i], ls[i]));
+    for (int i = 0; i < gr.G; ++i) HIPCHK(hipGraphLaunch(it->second.execs[i], ls[i]));
   if (time_graph) {
     float ms = 0.0f;
     HIPCHK(hipEventRecord(tg1, ls[0]));
@@ -1339,15 +1405,15 @@ int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
       HIPCHK(hipEventRecord(mm->ev_out[i], ls[i]));
       HIPCHK(hipStreamWaitEvent(st, mm->ev_out[i], 0));
     }
+  // completion marker of this entry's replays (after the join: covers every sub-batch)
+  if (!it->second.done) HIPCHK(hipEventCreateWithFlags(&it->second.done, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(it->second.done, st));
   return QTX_OK;
 }
 
-int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t* src_mask,
-                          int32_t B, int32_t S, int32_t max_len, int64_t start, int64_t* ids,
-                          void* ws, size_t ws_bytes, void* stream) {
-  return qtx_greedy_decode_fault(m, src, src_mask, B, S, max_len, start, ids, ws, ws_bytes,
-                                 nullptr, stream);
-}
+}  // namespace
+
+extern "C" {
 
 // ---- per-op entry points ---------------------------------------------------------------
 int32_t qtx_row_quant(const float* x, int32_t rows, int32_t D, float qmax, int8_t* q,

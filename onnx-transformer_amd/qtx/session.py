@@ -147,14 +147,21 @@ def run_module(module, input_values, module_filepath=None, module_weight_dict=No
     kind = _module_kind(module)
     fn = run_encoder if kind == "encoder" else run_decoder
     flt = None
+    if inject_parameters and not isinstance(inject_parameters, F.Fault):
+        # INPUT / WEIGHT kinds are injected only into the module they target
+        # (onnx_optimized_inference.py:74: `module in inject_parameters["targetted_module"]`);
+        # RANDOM kinds match the node name alone (:59), i.e. the module being run
+        kind_ = inject_parameters["inject_type"]
+        targetted = str(inject_parameters.get("targetted_module", module))
+        if "RANDOM" not in kind_ and str(module) not in targetted:
+            inject_parameters = None
     if inject_parameters:
         if isinstance(inject_parameters, F.Fault):
             flt = inject_parameters
         else:
             x = input_values["global_in"]
             rows = int(np.prod(_shape(x)[:2]))
-            mod, _, lin = F.matmul_target(inject_parameters["faulty_operation_name"],
-                                          inject_parameters.get("targetted_module", kind))
+            mod, _, lin = F.matmul_target(inject_parameters["faulty_operation_name"], kind)
             if lin in ("CK", "CV"):
                 rows = int(np.prod(_shape(input_values["global_in_1"])[:2]))
             golden = None

@@ -13,7 +13,15 @@ import socket
 import numpy as np
 import pytest
 
-from qtx.decode import make_src_mask, shard_bounds
+from qtx.decode import length_sorted_shards, make_src_mask, shard_bounds
+
+
+def test_length_sorted_shards():
+    lens = np.array([5, 9, 9, 2, 7, 12, 3])
+    sh = length_sorted_shards(lens, 3)
+    assert sorted(np.concatenate(sh).tolist()) == list(range(7))
+    assert [len(s) for s in sh] == [3, 2, 2]
+    assert sh[0].tolist() == [5, 1, 2] and sh[1].tolist() == [4, 0]   # longest first, stable
 
 
 def test_shard_bounds_partition():
@@ -50,7 +58,7 @@ def _rank(rank, world, port, out_dir):
     import torch
     import torch.distributed as dist
     from oracle.qtx_oracle import OracleModel
-    from qtx.decode import make_src_mask, shard_bounds
+    from qtx.decode import gather_ids, length_sorted_shards, make_src_mask
     from qtx.weights import ModelConfig, synthetic_state_dict
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
@@ -58,21 +66,13 @@ def _rank(rank, world, port, out_dir):
     cfg = ModelConfig(n_layers=2)
     om = OracleModel(synthetic_state_dict(20241223, cfg), n_layers=2)
     src = _batch()
-    lo, hi = shard_bounds(len(src), world, rank)
-    ys = om.greedy_decode(src[lo:hi], make_src_mask(src[lo:hi]), 6)
-    # gather variable-size shards: pad to the largest shard
-    n = torch.tensor([hi - lo])
-    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    mx = int(max(s.item() for s in sizes))
-    buf = torch.full((mx, 6), -1, dtype=torch.int64)
-    buf[:hi - lo] = torch.from_numpy(ys)
-    parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf)
+    # bench.py's partition and gather: length-sorted shards, padded all_gather
+    idx = length_sorted_shards((src != 2).sum(1), world)[rank]
+    ys = om.greedy_decode(src[idx], make_src_mask(src[idx]), 6)
+    full = gather_ids(dist, torch.from_numpy(ys), idx, len(src), world)
     t = torch.tensor([float(rank + 1)])
     dist.all_reduce(t, op=dist.ReduceOp.MAX)                 # bench.py's max-over-ranks
     if rank == 0:
-        full = np.concatenate([p[:int(s.item())].numpy() for p, s in zip(parts, sizes)])
         np.save(os.path.join(out_dir, "sharded.npy"), full)
         np.save(os.path.join(out_dir, "tmax.npy"), t.numpy())
     dist.destroy_process_group()
