@@ -45,5 +45,25 @@ def main(d):
               f"{100 * r['total_ns'] / tot:.1f} |")
 
 
+def by_grid(d, top=40):
+    """Second table: the same dispatches split by launch grid (one kernel at several
+    shapes — e.g. the decode GEMMs at B=32 and B=256 — averaged separately)."""
+    dbs = sorted(glob.glob(os.path.join(d, "**", "*.db"), recursive=True))
+    if not dbs:
+        return
+    c = sqlite3.connect(dbs[0])
+    rows = c.execute("select name, grid_x, grid_y, workgroup_x, count(*), sum(duration), "
+                     "avg(duration), min(duration), max(duration) from kernels "
+                     "group by name, grid_x, grid_y, workgroup_x order by sum(duration) desc "
+                     f"limit {top}").fetchall()
+    print("\n### by launch grid (grid = threads, x * y)\n")
+    print("| kernel | grid | calls | total us | avg us | min us | max us |")
+    print("|---|---|---:|---:|---:|---:|---:|")
+    for n, gx, gy, wx, cnt, tot, avg, mn, mx in rows:
+        print(f"| `{n[:90]}` | {gx}x{gy} (wg {wx}) | {cnt} | {tot / 1e3:.1f} | {avg / 1e3:.2f} | "
+              f"{mn / 1e3:.2f} | {mx / 1e3:.2f} |")
+
+
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof")
+    by_grid(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof")
