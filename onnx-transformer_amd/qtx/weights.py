@@ -146,12 +146,15 @@ def synthetic_state_dict(seed: int = DEFAULT_SEED, cfg: ModelConfig = ModelConfi
     return sd
 
 
-def load_checkpoint(path: str) -> dict:
+def load_checkpoint(path: str, smooth_scales: str | dict | None = None,
+                    alpha: float = 0.5) -> dict:
     """Load a reference ``state_dict`` checkpoint without executing pickled code.
 
     Uses ``torch.load(weights_only=True)``; keys must match :func:`tensor_order`.
-    Smoothing is *not* applied: ``output.py:609-613`` calls ``get_quantized`` before
-    ``load_state_dict``, which overwrites the smoothed tensors.
+    By default smoothing is *not* applied: ``output.py:609-613`` calls ``get_quantized``
+    before ``load_state_dict``, which overwrites the smoothed tensors.
+    ``smooth_scales`` (a path for :func:`load_act_scales` or its dict) opts in to the
+    SmoothQuant fold (:func:`smooth_state_dict`).
     """
     import torch
 
@@ -160,4 +163,78 @@ def load_checkpoint(path: str) -> dict:
     missing = [k for k in tensor_order() if k not in sd]
     if missing:
         raise KeyError(f"checkpoint {path} lacks {len(missing)} tensors, e.g. {missing[:3]}")
+    if smooth_scales is not None:
+        sc = load_act_scales(smooth_scales) if isinstance(smooth_scales, str) else smooth_scales
+        sd = smooth_state_dict(sd, sc, alpha)
     return sd
+
+
+# --------------------------------------------------------------------------------------
+# SmoothQuant fold (opt-in)
+# --------------------------------------------------------------------------------------
+
+def smooth_groups(cfg: ModelConfig = ModelConfig()) -> list[tuple[str, list[str], str]]:
+    """(LayerNorm, linears it feeds, act-scale key) triples that ``smooth_lm``
+    (get_quantized_model.py:46-148) smooths, in its module order:
+
+    * encoder layer L: sublayer.0.norm -> self_attn Q/K/V (scales of ``linears.0``),
+      sublayer.1.norm -> feed_forward.w_1;
+    * decoder layer L: sublayer.0.norm -> self_attn Q/K/V; sublayer.1.norm -> src_attn
+      Q/K/V; sublayer.2.norm -> feed_forward.w_1.
+
+    As in the reference, the src_attn K/V weights are scaled too although their input is
+    the encoder memory, not that LayerNorm's output (get_quantized_model.py:126-133)."""
+    g = []
+    for L in range(cfg.n_layers):
+        p = f"encoder.layers.{L}"
+        g.append((f"{p}.sublayer.0.norm", [f"{p}.self_attn.linears.{i}" for i in range(3)],
+                  f"{p}.self_attn.linears.0"))
+        g.append((f"{p}.sublayer.1.norm", [f"{p}.feed_forward.w_1"], f"{p}.feed_forward.w_1"))
+    for L in range(cfg.n_layers):
+        p = f"decoder.layers.{L}"
+        g.append((f"{p}.sublayer.0.norm", [f"{p}.self_attn.linears.{i}" for i in range(3)],
+                  f"{p}.self_attn.linears.0"))
+        g.append((f"{p}.sublayer.1.norm", [f"{p}.src_attn.linears.{i}" for i in range(3)],
+                  f"{p}.src_attn.linears.0"))
+        g.append((f"{p}.sublayer.2.norm", [f"{p}.feed_forward.w_1"], f"{p}.feed_forward.w_1"))
+    return g
+
+
+def load_act_scales(path: str) -> dict:
+    """The per-channel activation maxima SmoothQuant uses (the reference's
+    ``scales/transformer_scales.pt``, a dict of fp32 vectors keyed by linear name), loaded
+    without executing pickled code (torch.load weights_only=True), or from an .npz."""
+    if path.endswith(".npz"):
+        with np.load(path) as z:
+            return {k: np.asarray(z[k], np.float32) for k in z.files}
+    import torch
+    raw = torch.load(path, map_location="cpu", weights_only=True)
+    return {k: v.detach().float().numpy() for k, v in raw.items()}
+
+
+def smooth_state_dict(sd: dict, act_scales: dict, alpha: float = 0.5,
+                      cfg: ModelConfig = ModelConfig()) -> dict:
+    """SmoothQuant folded into the weights at load (smooth_ln_fcs, get_quantized_model.py:
+    9-36, applied as smooth_lm does, :46-148): per input channel j of each group,
+    ``s_j = clamp(act_max_j^alpha / clamp(max_i |W_ij|, 1e-5)^(1-alpha), 1e-5)`` with the
+    weight maximum over all of the group's linears; ``a_2 /= s``, ``b_2 /= s``,
+    ``W[:, j] *= s_j``.  Same torch fp32 ops as the reference, so the folded tensors are
+    bit-identical to a smoothed reference model's.
+
+    Opt-in: the reference's exported path loads its checkpoint *after* smoothing, which
+    undoes it (output.py:609-613), so the default load applies nothing.
+    Returns a new dict; ``sd`` is not modified."""
+    import torch
+
+    out = dict(sd)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32))
+    for ln, fcs, key in smooth_groups(cfg):
+        ws = [T(out[f"{n}.weight"]) for n in fcs]
+        wmax = torch.cat([w.abs().max(dim=0, keepdim=True)[0] for w in ws], dim=0)
+        wmax = wmax.max(dim=0)[0].clamp(min=1e-5)
+        s = (T(act_scales[key]).pow(alpha) / wmax.pow(1 - alpha)).clamp(min=1e-5)
+        out[f"{ln}.a_2"] = T(out[f"{ln}.a_2"]).div(s).numpy()
+        out[f"{ln}.b_2"] = T(out[f"{ln}.b_2"]).div(s).numpy()
+        for n, w in zip(fcs, ws):
+            out[f"{n}.weight"] = w.mul(s.view(1, -1)).numpy()
+    return out
