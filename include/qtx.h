@@ -74,6 +74,20 @@ int32_t qtx_model_destroy(qtx_model* m);
 /* bytes of device memory owned by the model */
 size_t qtx_model_device_bytes(const qtx_model* m);
 
+/* Read-only views of the model's device tensors, for the op-by-op traced executor
+ * (qtx/trace.py: the reference's node-by-node executor storing every intermediate by
+ * name, onnx_optimized_inference.py:32-57).  module 0 = encoder, 1 = decoder; index in the
+ * layer's weights.py:linear_names order (encoder 0..3 self_attn.linears, 4 w_1, 5 w_2;
+ * decoder 0..3 self_attn, 4..7 src_attn, 8 w_1, 9 w_2).  q: int8 [N,K] (weight_bits 4:
+ * packed [N,K/2]), s [N], b [N]: the per-channel quantized weight (quant_linear.py:5-17). */
+int32_t qtx_model_linear(const qtx_model* m, int32_t module, int32_t layer, int32_t index,
+                         const void** q, const float** s, const float** b, int32_t* N,
+                         int32_t* K);
+/* LayerNorm a_2 / b_2 [d_model]: sublayer index within the layer, or layer = -1 for the
+ * stack's final norm (encoder.py:18, decoder.py:16). */
+int32_t qtx_model_norm(const qtx_model* m, int32_t module, int32_t layer, int32_t sub,
+                       const float** a, const float** b);
+
 /* Workspace sizes (bytes) for the model-level calls. */
 size_t qtx_encoder_workspace_size(const qtx_model* m, int32_t B, int32_t S);
 size_t qtx_decoder_workspace_size(const qtx_model* m, int32_t B, int32_t T, int32_t S);

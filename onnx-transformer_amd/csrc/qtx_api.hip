@@ -353,6 +353,68 @@ int32_t qtx_model_destroy(qtx_model* m) {
 
 size_t qtx_model_device_bytes(const qtx_model* m) { return m ? m->bytes : 0; }
 
+int32_t qtx_model_linear(const qtx_model* m, int32_t module, int32_t layer, int32_t index,
+                         const void** q, const float** s, const float** b, int32_t* N,
+                         int32_t* K) {
+  if (!m || !q || !s || !b || !N || !K) return fail(QTX_E_INVALID, "qtx_model_linear: null argument");
+  if (layer < 0 || layer >= m->cfg.n_layers) return fail(QTX_E_INVALID, "layer %d out of range", layer);
+  // a slice of `rows` output channels starting at `r0` of a stored (possibly concatenated) linear
+  auto view = [&](const QLin& l, int r0, int rows) {
+    const long rb = m->cfg.weight_bits == 4 ? l.K / 2 : l.K;   // bytes per weight row
+    *q = l.q + (long)r0 * rb;
+    *s = l.s + r0;
+    *b = l.b + r0;
+    *N = rows;
+    *K = l.K;
+    return (int32_t)QTX_OK;
+  };
+  const int D = m->cfg.d_model;
+  if (module == 0) {
+    const EncLayer& e = m->enc[layer];
+    switch (index) {
+      case 0: case 1: case 2: return view(e.qkv, index * D, D);
+      case 3: return view(e.o, 0, e.o.N);
+      case 4: return view(e.w1, 0, e.w1.N);
+      case 5: return view(e.w2, 0, e.w2.N);
+    }
+  } else if (module == 1) {
+    const DecLayer& d = m->dec[layer];
+    switch (index) {
+      case 0: case 1: case 2: return view(d.qkv, index * D, D);
+      case 3: return view(d.o, 0, d.o.N);
+      case 4: return view(d.cq, 0, d.cq.N);
+      case 5: case 6: return view(d.ckv, (index - 5) * D, D);
+      case 7: return view(d.co, 0, d.co.N);
+      case 8: return view(d.w1, 0, d.w1.N);
+      case 9: return view(d.w2, 0, d.w2.N);
+    }
+  }
+  return fail(QTX_E_INVALID, "qtx_model_linear: no linear %d of module %d", index, module);
+}
+
+int32_t qtx_model_norm(const qtx_model* m, int32_t module, int32_t layer, int32_t sub,
+                       const float** a, const float** b) {
+  if (!m || !a || !b) return fail(QTX_E_INVALID, "qtx_model_norm: null argument");
+  if (layer == -1 && (module == 0 || module == 1)) {
+    const float* const* n = module == 0 ? m->enc_norm : m->dec_norm;
+    *a = n[0];
+    *b = n[1];
+    return QTX_OK;
+  }
+  if (layer < 0 || layer >= m->cfg.n_layers) return fail(QTX_E_INVALID, "layer %d out of range", layer);
+  if (module == 0 && sub >= 0 && sub < 2) {
+    *a = m->enc[layer].ln[sub][0];
+    *b = m->enc[layer].ln[sub][1];
+    return QTX_OK;
+  }
+  if (module == 1 && sub >= 0 && sub < 3) {
+    *a = m->dec[layer].ln[sub][0];
+    *b = m->dec[layer].ln[sub][1];
+    return QTX_OK;
+  }
+  return fail(QTX_E_INVALID, "qtx_model_norm: no norm %d of module %d layer %d", sub, module, layer);
+}
+
 }  // extern "C"
 
 // =======================================================================================

@@ -58,6 +58,9 @@ SIGNATURES = {
     "qtx_model_create": (I32, [C.POINTER(QtxConfig), C.POINTER(P), I32, P, P, C.POINTER(P)]),
     "qtx_model_destroy": (I32, [P]),
     "qtx_model_device_bytes": (SZ, [P]),
+    "qtx_model_linear": (I32, [P, I32, I32, I32, C.POINTER(P), C.POINTER(P), C.POINTER(P),
+                               C.POINTER(I32), C.POINTER(I32)]),
+    "qtx_model_norm": (I32, [P, I32, I32, I32, C.POINTER(P), C.POINTER(P)]),
     "qtx_encoder_workspace_size": (SZ, [P, I32, I32]),
     "qtx_decoder_workspace_size": (SZ, [P, I32, I32, I32]),
     "qtx_greedy_workspace_size": (SZ, [P, I32, I32, I32]),

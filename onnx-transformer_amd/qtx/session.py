@@ -60,8 +60,10 @@ def _shape(a):
     return tuple(a.shape)
 
 
-def run_encoder(model: QtxModel, feeds: dict, fault=None):
-    """global_in f32 [B,S,512], global_in_1 bool [B,1,S] -> global_out f32 [B,S,512]."""
+def run_encoder(model: QtxModel, feeds: dict, fault=None, trace=None):
+    """global_in f32 [B,S,512], global_in_1 bool [B,1,S] -> global_out f32 [B,S,512].
+    trace: None (the fused forward) or a dict that the op-by-op traced executor
+    (qtx.trace) fills with the named intermediates ("weights": the weight codes too)."""
     import torch
     _check(feeds, ENCODER_FEEDS)
     x, m = feeds["global_in"], feeds["global_in_1"]
@@ -72,10 +74,16 @@ def run_encoder(model: QtxModel, feeds: dict, fault=None):
         raise ValueError(f"global_in_1: expected [B,1,S]=[{B},1,{S}], got {_shape(m)}")
     xd = _as_torch(x, model.device, torch.float32)
     md = to_u8_mask(m, model.device).reshape(B, S)
+    if trace is not None:
+        from .trace import trace_encoder
+        with torch.cuda.device(model.device):
+            out, names = trace_encoder(model, xd, md, weights=bool(trace.pop("weights", False)))
+        trace.update(names)
+        return out
     return model.encode(xd, md, fault=fault)
 
 
-def run_decoder(model: QtxModel, feeds: dict, fault=None):
+def run_decoder(model: QtxModel, feeds: dict, fault=None, trace=None):
     """global_in [B,T,512], global_in_1 memory [B,S,512], global_in_2 [B,1,S],
     global_in_3 int64 [1,T,T] (or [B,T,T]) -> global_out [B,T,512]."""
     import torch
@@ -97,6 +105,13 @@ def run_decoder(model: QtxModel, feeds: dict, fault=None):
     smd = to_u8_mask(sm, model.device).reshape(B, S)
     tmd = to_u8_mask(tm, model.device)
     tmd = tmd.reshape(T, T) if int(np.prod(ts)) == T * T else tmd.reshape(B, T, T)
+    if trace is not None:
+        from .trace import trace_decoder
+        with torch.cuda.device(model.device):
+            out, names = trace_decoder(model, yd, md, smd, tmd,
+                                       weights=bool(trace.pop("weights", False)))
+        trace.update(names)
+        return out
     return model.decode(yd, md, smd, tmd, fault=fault)
 
 
@@ -129,8 +144,15 @@ class InferenceSession:
 
 def run_module(module, input_values, module_filepath=None, module_weight_dict=None,
                module_graph=None, inject_parameters=None, model: QtxModel | None = None,
-               rng=None):
+               rng=None, expose_intermediates=False):
     """onnx_optimized_inference.py:297-304 contract: returns (output_tensors, weight_dict).
+
+    expose_intermediates: True stores every quantizer's int8 codes (``Round_<n>_out0``,
+    float32 as the graph's Round nodes produce them, + ``Round_<n>_scale``) and every
+    QuantLinear MatMul's accumulators (``MatMul_<n>_out0``) in weight_dict under the
+    exported graph's names, as the reference's node-by-node executor does
+    (onnx_optimized_inference.py:57); "weights" adds the weight codes.  The module then
+    runs op by op (qtx.trace; same result bit for bit) instead of fused.
 
     inject_parameters: the reference's dict (inject_type INPUT/WEIGHT/INPUT16/WEIGHT16/
     RANDOM/RANDOM_BITFLIP, faulty_operation_name "MatMul_<n>", targetted_module,
@@ -173,6 +195,14 @@ def run_module(module, input_values, module_filepath=None, module_weight_dict=No
             flt = F.from_inject_parameters(dict(inject_parameters, targetted_module=kind), rows,
                                            rng, model.cfg.n_layers, golden, (B, Sq, Sk))
         weight_dict["qtx_fault"] = flt
+    if expose_intermediates:
+        if flt is not None:
+            raise ValueError("expose_intermediates runs the golden (fault-free) module only")
+        trace = {"weights": expose_intermediates == "weights"}
+        out = fn(model, input_values, None, trace).cpu().numpy()
+        weight_dict.update(trace)
+        weight_dict["global_out"] = out
+        return {"global_out": out}, weight_dict
     out = fn(model, input_values, flt).cpu().numpy()
     weight_dict["global_out"] = out
     return {"global_out": out}, weight_dict
