@@ -159,7 +159,7 @@ class _DevView:
 
     def __init__(self, ptr, shape, typestr):
         self.__cuda_array_interface__ = {"shape": shape, "typestr": typestr,
-                                         "data": (ptr, True), "version": 2}
+                                         "data": (ptr, False), "version": 2}
 
 
 def _view(torch, ptr, shape, typestr, device):
