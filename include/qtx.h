@@ -279,6 +279,15 @@ int32_t qtx_decode_attention(int32_t kv_new, const float* y, int64_t ldy, int8_t
                              const int32_t* step_dev, int32_t S, const uint8_t* mask,
                              int32_t B, float* ctx, float* pmax, void* stream);
 
+/* The decode step's tail (onnx_reference_inference.py:632,640-643): per row m of logits
+ * [M, tgt_vocab], the first argmax of log_softmax (generator.py:15, torch.max's tie rule)
+ * into ids[m * ids_bs + s + 1], and the next decoder input tgt_embed(id) at position s + 1
+ * into x_next [M, d_model], with s = step_dev[0]; step_dev[1] must be 0 (arrival counter);
+ * the last workgroup advances step_dev[0] by one. */
+int32_t qtx_decode_argmax_embed(const qtx_model* m, const float* logits, int32_t M,
+                                int64_t* ids, int64_t ids_bs, int32_t* step_dev,
+                                float* x_next, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1592,6 +1592,21 @@ int32_t qtx_decode_attention(int32_t kv_new, const float* y, int64_t ldy, int8_t
   return QTX_OK;
 }
 
+int32_t qtx_decode_argmax_embed(const qtx_model* m, const float* logits, int32_t M,
+                                int64_t* ids, int64_t ids_bs, int32_t* step_dev,
+                                float* x_next, void* stream) {
+  if (!m || !logits || !ids || !step_dev || !x_next) return fail(QTX_E_INVALID, "null argument");
+  if (M <= 0) return QTX_OK;
+  const qtx_config& c = m->cfg;
+  const hipError_t e = launch_argmax_embed(logits, M, c.tgt_vocab, ids, ids_bs, step_dev,
+                                           reinterpret_cast<unsigned*>(step_dev + 1),
+                                           m->tgt_lut, m->pe, c.max_len, x_next,
+                                           (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "tgt_vocab %d", c.tgt_vocab);
+  HIPCHK(e);
+  return QTX_OK;
+}
+
 int32_t qtx_pack_int4(const int8_t* q, int32_t N, int32_t K, uint8_t* packed, void* stream) {
   if (!q || !packed || K % 2) return fail(QTX_E_INVALID, "bad argument");
   HIPCHK(launch_pack_int4(q, N, K, packed, (hipStream_t)stream));

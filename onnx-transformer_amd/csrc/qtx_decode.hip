@@ -485,6 +485,7 @@ __global__ __launch_bounds__(256) void k_generator_mfma(const float* x, long ldx
   const int m0 = blockIdx.y * 16;
   const int vcol = blockIdx.x * 64 + 16 * wave + fr;
   const int vl = min(vcol, V - 1);
+  QTX_STAMP(0);
   float bq[2][32];
 #pragma unroll
   for (int s = 0; s < 32; ++s) bq[0][s] = Wt[(long)(4 * s + fg) * V + vl];
@@ -509,6 +510,7 @@ __global__ __launch_bounds__(256) void k_generator_mfma(const float* x, long ldx
       *reinterpret_cast<float2*>(d + 2) = make_float2(xv[j][c][2], xv[j][c][3]);
     }
   __syncthreads();
+  QTX_STAMP(1);
   v4f acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -523,12 +525,14 @@ __global__ __launch_bounds__(256) void k_generator_mfma(const float* x, long ldx
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bq[q & 1][s], acc, 0, 0, 0);
     }
   }
+  QTX_STAMP(2);
   if (vcol >= V) return;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int m = m0 + 4 * fg + e;
     if (m < M) logits[(long)m * V + vcol] = acc[e] + bv;
   }
+  QTX_STAMP(3);
 }
 
 hipError_t launch_generator_mfma(const float* x, long ldx, int M, const float* ln_a,
@@ -539,6 +543,14 @@ hipError_t launch_generator_mfma(const float* x, long ldx, int M, const float* l
       x, ldx, M, ln_a, ln_b, Wt, b, V, logits);
   return hipGetLastError();
 }
+
+#ifdef QTX_STAMPS   // diagnostic builds only: the generator launched bare (tools/stamp_bench.py)
+extern "C" int qtx_debug_generator(const float* x, int M, const float* lna, const float* lnb,
+                                   const float* Wt, const float* b, int V, float* logits,
+                                   void* st) {
+  return (int)launch_generator_mfma(x, 512, M, lna, lnb, Wt, b, V, logits, (hipStream_t)st);
+}
+#endif
 
 __global__ void k_transpose(const float* in, int R, int Cc, float* out) {
   __shared__ float t[32][33];
@@ -556,19 +568,37 @@ hipError_t launch_transpose(const float* in, int R, int Cc, float* out, hipStrea
 
 // =====================================================================================
 // k_argmax_embed: one 1024-thread workgroup per row.  The row of logits stays in
-// registers (8 per thread, all loads in flight at once); only the exponentials go through
-// LDS, for the canonical lane-split denominator (wave 0).  Then the first argmax of logp,
-// and the block writes the next decoder input.
+// registers (8 per thread, all loads in flight at once).  The token is the first argmax
+// of logp = (x - max) - lse (generator.py:15 log_softmax, torch.max's first-index rule).
+// lse only matters when another logit lies within a few ulps of the maximum: with
+// lse = logf(sum) <= logf(V) < 16, (x - max) < -ARG_DELTA rounds below -lse, so only
+// values above max - ARG_DELTA can tie it.  Fast path (block-uniform): exactly one such
+// value — it is the maximum and the token.  Otherwise the exponentials go through LDS
+// for the canonical lane-split denominator (wave 0) and the first argmax of logp decides.
+// Then the block writes the next decoder input (embedding + PE of the token).
 // =====================================================================================
 constexpr int ARG_T = 1024, ARG_NV = 8, ARG_MAXV = ARG_T * ARG_NV;
+constexpr float ARG_DELTA = 4.0e-6f;   // >= 2 ulp(16): covers every V <= ARG_MAXV
+
+__device__ __forceinline__ int wave_sum_i32(int v) {
+  auto d = [](int x, auto ctrl) {
+    return __builtin_amdgcn_update_dpp(0, x, decltype(ctrl)::value, 0xF, 0xF, true);
+  };
+  v += d(v, std::integral_constant<int, 0xB1>{});
+  v += d(v, std::integral_constant<int, 0x4E>{});
+  v += d(v, std::integral_constant<int, 0x141>{});
+  v += d(v, std::integral_constant<int, 0x140>{});
+  return (__builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16)) +
+         (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
+}
 
 __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int V, int64_t* ids,
                                                        long ids_bs, int* step, unsigned* arrive,
                                                        const float* lut, const float* pe,
                                                        int max_pos, float* xnext) {
   __shared__ float Ev[ARG_MAXV];
-  __shared__ float red[16], redv[16], lse_s;
-  __shared__ int redi[16], bsh;
+  __shared__ float redf[16], lse_s;
+  __shared__ int redi[16], redc[16];
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   QTX_STAMP(0);
   const int s = *step;
@@ -579,65 +609,76 @@ __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int 
 #pragma unroll
   for (int i = 0; i < ARG_NV; ++i) t[i] = x[min(tid + ARG_T * i, V - 1)];   // clamped
   QTX_STAMP(1);
-  // max: order-free
+  // max: order-free; every wave reduces the 16 wave maxima itself (no second barrier)
   float lm = -3.0e38f;
 #pragma unroll
   for (int i = 0; i < ARG_NV; ++i)
     if (tid + ARG_T * i < V) lm = fmaxf(lm, t[i]);
   lm = wave_max(lm);
-  if (lane == 0) red[w] = lm;
+  if (lane == 0) redf[w] = lm;
   __syncthreads();
-  float mx = red[0];
-#pragma unroll
-  for (int i = 1; i < 16; ++i) mx = fmaxf(mx, red[i]);
-  // e_v = qexp(x_v - max) into LDS for the ordered sum
-#pragma unroll
-  for (int i = 0; i < ARG_NV; ++i) {
-    const int v = tid + ARG_T * i;
-    if (v < V) Ev[v] = qexp(t[i] - mx);
-  }
-  __syncthreads();
-  QTX_STAMP(2);
-  // canonical denominator: lane l sums e[l], e[l+64], ... in order (one wave), then tree
-  if (w == 0) {
-    float ls = 0.0f;
-#pragma unroll 8
-    for (int v = lane; v < V; v += 64) ls = ls + Ev[v];
-    ls = wave_sum(ls);
-    if (lane == 0) lse_s = logf(ls);
-  }
-  __syncthreads();
-  const float lse = lse_s;
-  QTX_STAMP(3);
-  // first argmax of logp = (x - max) - lse (torch.max tie rule)
-  float best = -3.0e38f;
-  int bi = 0x7fffffff;
+  const float mx = wave_max(lane < 16 ? redf[lane] : -3.0e38f);
+  // candidates for the first argmax of logp, and the first index of the maximum
+  int cnt = 0, bi = 0x7fffffff;
 #pragma unroll
   for (int i = 0; i < ARG_NV; ++i) {
     const int v = tid + ARG_T * i;
     if (v < V) {
-      const float lp = (t[i] - mx) - lse;
-      if (lp > best) { best = lp; bi = v; }
+      cnt += t[i] > mx - ARG_DELTA ? 1 : 0;
+      if (t[i] == mx && v < bi) bi = v;
     }
   }
-  // wave: the maximum, then the smallest index holding it (DPP trees, no LDS round trips)
-  const float wb = wave_max(best);
-  const int wi = wave_min_i32(best == wb ? bi : 0x7fffffff);
-  if (lane == 0) { redv[w] = wb; redi[w] = wi; }
+  cnt = wave_sum_i32(cnt);
+  bi = wave_min_i32(bi);
+  if (lane == 0) { redc[w] = cnt; redi[w] = bi; }
   __syncthreads();
-  if (tid == 0) {
-    best = redv[0]; bi = redi[0];
-    for (int k = 1; k < 16; ++k)
-      if (redv[k] > best || (redv[k] == best && redi[k] < bi)) { best = redv[k]; bi = redi[k]; }
-    bi = min(bi, V - 1);   // all-NaN row guard: keep the embedding gather in bounds
-    ids[m * ids_bs + s + 1] = bi;
-    bsh = bi;
+  cnt = wave_sum_i32(lane < 16 ? redc[lane] : 0);
+  int id = wave_min_i32(lane < 16 ? redi[lane] : 0x7fffffff);
+  QTX_STAMP(2);
+  if (cnt != 1) {   // near-tie (or non-finite row): the exact log-softmax decides (block-uniform)
+    // e_v = qexp(x_v - max) into LDS for the ordered sum
+#pragma unroll
+    for (int i = 0; i < ARG_NV; ++i) {
+      const int v = tid + ARG_T * i;
+      if (v < V) Ev[v] = qexp(t[i] - mx);
+    }
+    __syncthreads();
+    // canonical denominator: lane l sums e[l], e[l+64], ... in order (one wave), then tree
+    if (w == 0) {
+      float ls = 0.0f;
+#pragma unroll 8
+      for (int v = lane; v < V; v += 64) ls = ls + Ev[v];
+      ls = wave_sum(ls);
+      if (lane == 0) lse_s = logf(ls);
+    }
+    __syncthreads();
+    const float lse = lse_s;
+    // first argmax of logp = (x - max) - lse (torch.max tie rule)
+    float best = -3.0e38f;
+    int bj = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < ARG_NV; ++i) {
+      const int v = tid + ARG_T * i;
+      if (v < V) {
+        const float lp = (t[i] - mx) - lse;
+        if (lp > best) { best = lp; bj = v; }
+      }
+    }
+    // the maximum, then the smallest index holding it: per wave, then over the 16 waves
+    const float wb = wave_max(best);
+    const int wi = wave_min_i32(best == wb ? bj : 0x7fffffff);
+    __syncthreads();                       // (redf / redi are reused)
+    if (lane == 0) { redf[w] = wb; redi[w] = wi; }
+    __syncthreads();
+    const float gv = lane < 16 ? redf[lane] : -3.0e38f;
+    const float gb = wave_max(gv);
+    id = wave_min_i32(lane < 16 && gv == gb ? redi[lane] : 0x7fffffff);
+    id = min(id, V - 1);                   // all-NaN row guard: keep the embedding gather in bounds
   }
-  __syncthreads();
+  if (tid == 0) ids[m * ids_bs + s + 1] = id;
   QTX_STAMP(4);
   // next decoder input: tgt_embed(id) at position s + 1 (embeddings.py:12-13)
   if (tid < 128) {
-    const int id = bsh;
     const float sc = 0x1.6a09e6p+4f;
     const float4 e = *reinterpret_cast<const float4*>(lut + (long)id * 512 + 4 * tid);
     const float4 q = pe_row;

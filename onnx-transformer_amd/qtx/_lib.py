@@ -83,6 +83,7 @@ SIGNATURES = {
     "qtx_skinny_linear": (I32, [I32, P, P, P, I64, P, P, P, I32, P, P, P, I32, I32, I32, I32,
                                 I32, P, P, P, P]),
     "qtx_decode_attention": (I32, [I32, P, I64, P, P, P, P, I32, P, I32, P, I32, P, P, P]),
+    "qtx_decode_argmax_embed": (I32, [P, P, I32, P, I64, P, P, P]),
 }
 
 

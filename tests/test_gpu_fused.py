@@ -178,3 +178,55 @@ def test_decode_cross_attention(torch, B, S):
     ctx, _ = O.attention(qq[:, None], sq[:, None], kc, skc, vc, svc, mask[:, None])
     np.testing.assert_array_equal(ctxd.cpu().numpy(), ctx[:, 0])
     np.testing.assert_array_equal(pm.cpu().numpy(), head_max(ctx[:, 0]))
+
+
+def oracle_first_argmax(logits):
+    """OracleModel.generator's token rule on given logits: first argmax of
+    (x - max) - lse with the canonical lane-split denominator."""
+    m = logits.max(axis=-1)
+    z = logits - m[:, None]
+    lse = np.log(O.row_sum_lanesplit(O.qexp(z))).astype(f32)
+    return (z - lse[:, None]).astype(f32).argmax(axis=-1)
+
+
+@pytest.mark.parametrize("case", ["random", "exact_ties", "near_ties", "collapse", "nan_rows"])
+def test_decode_argmax_embed(torch, gpu_model, oracle_model, case):
+    """The decode tail: fast path (one logit within 4e-6 of the max) and the exact
+    log-softmax path (ties, near-ties, values that round onto the max's log-prob,
+    non-finite rows) give the oracle's first-argmax token and its embedding."""
+    rng = np.random.default_rng(hash(case) % 1000)
+    M, V = 32, 4444
+    lg = (rng.standard_normal((M, V)) * 2).astype(f32)
+    if case == "exact_ties":
+        for r in range(M):
+            j = rng.integers(0, V, 3)
+            lg[r, j] = lg[r].max() + 1.0
+    elif case == "near_ties":
+        for r in range(M):
+            j = rng.integers(0, V, 2)
+            mx = lg[r].max() + 0.5
+            lg[r, j[0]] = mx
+            lg[r, j[1]] = np.nextafter(mx, f32(-np.inf)) if r % 2 else mx - f32(3e-6)
+    elif case == "collapse":          # many values within a few ulps: lse-rounding decides
+        for r in range(M):
+            mx = f32(rng.uniform(1, 6))
+            j = rng.choice(V, 6, replace=False)
+            lg[r, j] = mx - f32(1e-7) * rng.integers(0, 12, 6).astype(f32)
+    elif case == "nan_rows":
+        lg[0, :] = np.nan
+        lg[1, 5] = np.nan
+    ids = torch.zeros((M, 72), dtype=torch.int64, device="cuda")
+    step = torch.tensor([7, 0], dtype=torch.int32, device="cuda")
+    xn = torch.empty((M, 512), dtype=torch.float32, device="cuda")
+    call("qtx_decode_argmax_embed", gpu_model.handle, P(dev(torch, lg)), M, P(ids), 72, P(step),
+         P(xn), S0)
+    got = ids[:, 8].cpu().numpy()
+    want = oracle_first_argmax(lg)
+    if case == "nan_rows":                   # robustness only: ids stay in bounds
+        assert got[0] == V - 1 and (got >= 0).all() and (got < V).all()
+        got, want = got[2:], want[2:]
+    np.testing.assert_array_equal(got, want)
+    assert step.cpu().tolist() == [8, 0]
+    ids_all = ids[:, 8].cpu().numpy()
+    emb = oracle_model.embed(ids_all[:, None], oracle_model.tgt_lut, pos0=8)[:, 0]
+    np.testing.assert_array_equal(xn.cpu().numpy(), emb)
