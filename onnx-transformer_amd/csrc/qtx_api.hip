@@ -101,7 +101,7 @@ struct qtx_model {
   const float* enc_norm[2];
   const float* dec_norm[2];
   const float *src_lut, *tgt_lut, *pe, *gen_w, *gen_b;
-  float* gen_wt = nullptr;   // generator weight transposed [d_model][tgt_vocab]
+  float* gen_wt = nullptr;   // generator weight in k_generator_mfma's MFMA order (pack_gen)
   void* mem = nullptr;
   size_t bytes = 0;
   // decode-step graphs, keyed by shape and the buffers baked into them
@@ -240,7 +240,7 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     float* gw = ar.take<float>((size_t)c.tgt_vocab * D);
     float* gb = ar.take<float>(c.tgt_vocab);
     int8_t* tmp = ar.take<int8_t>((size_t)F * D);
-    m->gen_wt = ar.take<float>((size_t)c.tgt_vocab * D);
+    m->gen_wt = ar.take<float>((size_t)((c.tgt_vocab + 15) / 16) * 16 * D);
     return std::make_tuple(norms, src_lut, tgt_lut, pe_d, gw, gb, tmp);
   };
   qtx_model* m = new qtx_model();
@@ -322,8 +322,8 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     if (he != hipSuccess) { qtx_model_destroy(m); return fail(QTX_E_HIP, "copy tables"); }
   }
   m->src_lut = src_lut; m->tgt_lut = tgt_lut; m->pe = pe_d; m->gen_w = gw; m->gen_b = gb;
-  he = launch_transpose(gw, c.tgt_vocab, D, m->gen_wt, st);
-  if (he != hipSuccess) { qtx_model_destroy(m); return fail(QTX_E_HIP, "transpose generator"); }
+  he = launch_pack_gen(gw, c.tgt_vocab, m->gen_wt, st);
+  if (he != hipSuccess) { qtx_model_destroy(m); return fail(QTX_E_HIP, "pack generator"); }
   he = hipStreamSynchronize(st);
   if (he != hipSuccess) {
     qtx_model_destroy(m);

@@ -471,25 +471,38 @@ hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st) {
 // v_mfma_f32_16x16x4_f32 chained over k = 0..511 (128 instructions, C starts at 0) is
 // bit-for-bit the k-ordered fmaf chain (cdna_hip_programming.md §3 "FP32-input MFMA"),
 // so logits[m, v] = (fma chain of x[m,k] * W[v,k]) + b[v] exactly as the oracle.
-// Block = 16 token rows x 64 vocab columns (4 waves, 16 columns each).  A operand =
-// the LayerNormed rows in LDS; B operand = Wt [512][V] (the generator weight stored
-// transposed at load), lane l reading Wt[4s + (l>>4)][v0 + (l&15)].
+// Block = 16 token rows x 64 vocab columns (4 waves, one 16-column strip each).  A operand
+// = the LayerNormed rows in LDS; B operand = the weight packed at load in MFMA order
+// (k_pack_gen: per strip, per group of 4 k-steps, per lane one float4), so each wave
+// streams its whole 32 KB strip with 32 coalesced 1 KB loads issued before the LayerNorm.
+// The two 16-row blocks of a strip group run on one XCD (blockIdx remap): the second
+// reads the strip from that XCD's L2.
 // =====================================================================================
+constexpr int GEN_Q = 32;   // float4 groups of 4 k-steps per lane (K = 512)
+
 __global__ __launch_bounds__(256) void k_generator_mfma(const float* x, long ldx, int M,
                                                         const float* ln_a, const float* ln_b,
-                                                        const float* Wt, const float* bias,
+                                                        const float* Wm, const float* bias,
                                                         int V, float* logits) {
   __shared__ __attribute__((aligned(16))) float X[16][514];   // stride 514: conflict-free reads
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
-  const int m0 = blockIdx.y * 16;
-  const int vcol = blockIdx.x * 64 + 16 * wave + fr;
-  const int vl = min(vcol, V - 1);
+  // blockIdx -> (strip group g, row block rb): hw = 8 (nrb (g / 8) + rb) + g % 8, so the
+  // row blocks of group g share hw % 8 (one XCD under round-robin placement)
+  const int nrb = (M + 15) / 16, hw = blockIdx.x;
+  const int rb = (hw >> 3) % nrb, g = ((hw >> 3) / nrb) * 8 + (hw & 7);
+  const int nstrip = (V + 15) / 16, strip = g * 4 + wave;
+  if (g * 4 >= nstrip) return;                     // whole block (uniform)
+  const int m0 = rb * 16;
+  const int vcol = strip * 16 + fr;
   QTX_STAMP(0);
-  float bq[2][32];
+  // 1. the strip's B operands, all in flight before anything else
+  const float4* wp = reinterpret_cast<const float4*>(Wm) + ((long)min(strip, nstrip - 1) * GEN_Q) * 64 + lane;
+  float4 wq[GEN_Q];
 #pragma unroll
-  for (int s = 0; s < 32; ++s) bq[0][s] = Wt[(long)(4 * s + fg) * V + vl];
-  const float bv = bias[vl];
+  for (int q = 0; q < GEN_Q; ++q) wq[q] = wp[q * 64];
+  const float bv = bias[min(vcol, V - 1)];
+  // 2. 16 rows (4 per wave), LayerNorm in the canonical order, into LDS
   float xv[4][2][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -511,18 +524,15 @@ __global__ __launch_bounds__(256) void k_generator_mfma(const float* x, long ldx
     }
   __syncthreads();
   QTX_STAMP(1);
+  // 3. the k-ordered chain: step s = 4q + e uses A = X[fr][4s + fg], B = wq[q][e]
   v4f acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    if (q + 1 < 4) {
+  for (int q = 0; q < GEN_Q; ++q) {
+    const float b4[4] = {wq[q].x, wq[q].y, wq[q].z, wq[q].w};
 #pragma unroll
-      for (int s = 0; s < 32; ++s)
-        bq[(q + 1) & 1][s] = Wt[(long)(4 * (32 * (q + 1) + s) + fg) * V + vl];
-    }
-#pragma unroll
-    for (int s = 0; s < 32; ++s) {
-      const float a = X[fr][4 * (32 * q + s) + fg];
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bq[q & 1][s], acc, 0, 0, 0);
+    for (int e = 0; e < 4; ++e) {
+      const float a = X[fr][4 * (4 * q + e) + fg];
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b4[e], acc, 0, 0, 0);
     }
   }
   QTX_STAMP(2);
@@ -536,11 +546,32 @@ __global__ __launch_bounds__(256) void k_generator_mfma(const float* x, long ldx
 }
 
 hipError_t launch_generator_mfma(const float* x, long ldx, int M, const float* ln_a,
-                                 const float* ln_b, const float* Wt, const float* b, int V,
+                                 const float* ln_b, const float* Wm, const float* b, int V,
                                  float* logits, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  k_generator_mfma<<<dim3((V + 63) / 64, (M + 15) / 16), dim3(256), 0, st>>>(
-      x, ldx, M, ln_a, ln_b, Wt, b, V, logits);
+  const int ngroup = (V + 63) / 64, nrb = (M + 15) / 16;
+  const unsigned grid = 8u * nrb * ((ngroup + 7) / 8);
+  k_generator_mfma<<<dim3(grid), dim3(256), 0, st>>>(x, ldx, M, ln_a, ln_b, Wm, b, V, logits);
+  return hipGetLastError();
+}
+
+// W [V][512] -> the MFMA-ordered strips of k_generator_mfma: out[((c * 32 + q) * 64 + l) * 4 + e]
+// = W[16 c + (l & 15)][4 (4 q + e) + (l >> 4)] (0 past V).  One thread per float4.
+__global__ void k_pack_gen(const float* W, int V, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nstrip = (V + 15) / 16;
+  if (i >= (long)nstrip * GEN_Q * 64) return;
+  const int l = (int)(i % 64), q = (int)((i / 64) % GEN_Q), c = (int)(i / (64 * GEN_Q));
+  const int v = 16 * c + (l & 15);
+  float4 o;
+  float* op = reinterpret_cast<float*>(&o);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) op[e] = v < V ? W[(long)v * 512 + 4 * (4 * q + e) + (l >> 4)] : 0.0f;
+  reinterpret_cast<float4*>(out)[i] = o;
+}
+hipError_t launch_pack_gen(const float* W, int V, float* out, hipStream_t st) {
+  const long n = (long)((V + 15) / 16) * GEN_Q * 64;
+  k_pack_gen<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(W, V, out);
   return hipGetLastError();
 }
 

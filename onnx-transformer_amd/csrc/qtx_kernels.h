@@ -156,6 +156,7 @@ hipError_t launch_generator_mfma(const float* x, long ldx, int M, const float* l
                                  const float* ln_b, const float* Wt, const float* b, int V,
                                  float* logits, hipStream_t st);
 hipError_t launch_transpose(const float* in, int R, int C, float* out, hipStream_t st);
+hipError_t launch_pack_gen(const float* W, int V, float* out, hipStream_t st);
 // log_softmax + argmax + next-token embedding + step increment (decode tail):
 //   ids[m, *step + 1] = argmax;  xnext[m] = lut[id]*sqrt(512) + pe[*step + 1];
 //   the last workgroup to finish advances *step (arrive is its private counter).

@@ -63,7 +63,7 @@ def main():
     ctx = torch.empty((B, 512), device="cuda")
     pma = torch.empty((8, B), device="cuda")
     pmi = T(np.full((128, B), 3.0, np.float32))
-    gwt = T((rng.standard_normal((512, 4444)) * 0.03).astype(np.float32))
+    gwt = T((rng.standard_normal((4448, 512)) * 0.03).astype(np.float32))   # packed strips
     gb = T(np.zeros(4444, np.float32))
     lg = torch.empty((B, 4444), device="cuda")
     L.qtx_generator_stamp = raw.qtx_debug_generator
@@ -78,7 +78,7 @@ def main():
         "dec_attn cross": (lambda: L.qtx_decode_attention(0, P(y), 512, P(kc), P(vc), P(skc), P(svc), 72, S0, 72, P(mask), B, P(ctx), P(pma), S0), 8 * B, 5),
         "skinny I8 1536": (lambda: L.qtx_skinny_linear(0, P(a8), P(sa), S0, 512, S0, S0, S0, 0, P(W), P(sw), P(bias), B, 1536, 512, 8, 0, S0, P(out), S0, S0), 96 * B // 8, 4),
         "skinny LN 1536": (lambda: L.qtx_skinny_linear(1, S0, S0, P(x), 512, P(lna), P(lnb), S0, 0, P(W), P(sw), P(bias), B, 1536, 512, 8, 0, S0, P(out), S0, S0), 96 * B // 4, 4),
-        "generator 32x4444": (lambda: L.qtx_generator_stamp(P(x), B, P(lna), P(lnb), P(gwt), P(gb), 4444, P(lg), S0), 70 * 2, 4),
+        "generator 32x4444": (lambda: L.qtx_generator_stamp(P(x), B, P(lna), P(lnb), P(gwt), P(gb), 4444, P(lg), S0), 72 * 2, 4),
         "skinny F32Q 512x2048": (lambda: L.qtx_skinny_linear(2, S0, S0, P(h), 2048, S0, S0, P(pmi), 128, P(W2), P(sw), P(bias), B, 512, 2048, 8, 2, P(out), P(out), S0, S0), 32 * B // 4, 4),
     }
     for name, (fn, nblk, nst) in cases.items():
