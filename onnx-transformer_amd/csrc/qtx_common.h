@@ -98,6 +98,17 @@ __device__ __forceinline__ int wave_min_i32(int v) {
   return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
              min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
+__device__ __forceinline__ int wave_max_i32(int v) {
+  auto d = [](int x, auto ctrl) {
+    return __builtin_amdgcn_update_dpp(int(0x80000000), x, decltype(ctrl)::value, 0xF, 0xF, false);
+  };
+  v = max(v, d(v, std::integral_constant<int, 0xB1>{}));
+  v = max(v, d(v, std::integral_constant<int, 0x4E>{}));
+  v = max(v, d(v, std::integral_constant<int, 0x141>{}));
+  v = max(v, d(v, std::integral_constant<int, 0x140>{}));
+  return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
 
 // ---------------------------------------------------------------- canonical exp
 // qexp(): Cody-Waite reduction + degree-7 Taylor in Horner form with fma (7 fused steps

@@ -260,13 +260,14 @@ int env_rb(const char* name, int def) {   // experiment overrides (QTX_RB_*)
   const char* v = getenv(name);
   return v && *v ? atoi(v) : def;
 }
-// Rows per workgroup (decode step, M = 32, measured in bench.py): small row blocks spread
+// Rows per workgroup (decode step, M = 32, measured in bench.py; tools/rb_sweep.sh: the
+// K = 512 int8 / F32Q row block 8 -> 4 took the step 234.8 -> 230.3 us): small row blocks spread
 // the A-panel and weight reads over more CUs — each CU sustains only a few KB in flight,
 // so a latency-bound kernel is fastest when every workgroup touches ~10-40 KB.
 template <int WB>
 hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
   if (g.K == 512) {
-    static const int rb_i8 = env_rb("QTX_RB_I8_512", 8), rb_ln = env_rb("QTX_RB_LN", 4);
+    static const int rb_i8 = env_rb("QTX_RB_I8_512", 4), rb_ln = env_rb("QTX_RB_LN", 4);
     if (g.amode == A_I8) return skinny_rb<512, WB, A_I8>(g, g.M <= 4 ? 4 : rb_i8, st);
     if (g.amode == A_LN) return skinny_rb<512, WB, A_LN>(g, rb_ln, st);
     if (g.amode == A_F32Q) return skinny_rb<512, WB, A_F32Q>(g, g.M <= 4 ? 4 : rb_i8, st);
@@ -342,7 +343,15 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   const float k_own = KV_NEW ? yr[512 + h * 64 + lane] : 0.0f;
   const float v_own = KV_NEW ? yr[1024 + h * 64 + lane] : 0.0f;
   const int step = KV_NEW ? *a.step : 0;
-  const int Sk = KV_NEW ? step + 1 : a.S;
+  // cross: keys past the sentence's last unmasked one contribute exactly nothing (score
+  // -1e9 -> qexp 0 -> P 0, and fma(0, v, acc) == acc), so the key loops stop there; a
+  // fully masked row keeps all S keys (the reference's uniform softmax over -1e9 scores)
+  int Sk = KV_NEW ? step + 1 : a.S;
+  if constexpr (!KV_NEW) {
+    const int last = wave_max_i32(max(keep0 && lane < a.S ? lane + 1 : 0,
+                                      keep1 && lane + 64 < a.S ? lane + 65 : 0));
+    if (last > 0) Sk = last;
+  }
 
   // phase 1: per-token scales of q (and k, v) over the full 512-wide rows
   auto amax8 = [](const float4 (&v)[2]) {

@@ -158,8 +158,11 @@ def test_decode_self_attention(torch, B, step, kv_bs):
     np.testing.assert_array_equal(pm.cpu().numpy(), head_max(ctx[:, 0]))
 
 
-@pytest.mark.parametrize("B,S", [(2, 16), (32, 72), (5, 128), (3, 1), (2, 17)])
-def test_decode_cross_attention(torch, B, S):
+@pytest.mark.parametrize("B,S,holes", [(2, 16, 0), (32, 72, 0), (5, 128, 0), (3, 1, 0), (2, 17, 0),
+                                       (8, 72, 1)])
+def test_decode_cross_attention(torch, B, S, holes):
+    """Suffix masks (padding), and with holes: masked keys inside the sentence and a fully
+    masked row (the key loops stop after the last unmasked key, exactly)."""
     rng = np.random.default_rng(B + S)
     y = rng.standard_normal((B, 512)).astype(f32)
     kc = rng.integers(-127, 128, (B, S, 512)).astype(np.int8)
@@ -169,6 +172,10 @@ def test_decode_cross_attention(torch, B, S):
     mask = np.ones((B, S), np.uint8)
     for b in range(B):
         mask[b, rng.integers(1, S + 1):] = 0
+    if holes:
+        mask[:, 3:9:2] = 0
+        mask[1, :] = 0
+        mask[2, 70] = 1
     ctxd = torch.empty((B, 512), dtype=torch.float32, device="cuda")
     pm = torch.empty((8, B), dtype=torch.float32, device="cuda")
     call("qtx_decode_attention", 0, P(dev(torch, y)), 512, P(dev(torch, kc)), P(dev(torch, vc)),
