@@ -254,9 +254,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # RCCL ("nccl") in production: one rank per GPU.  QTX_BENCH_BACKEND=gloo rehearses the
+    # multi-rank flow (sharding, timing reduction, id gather, verification) with several
+    # ranks sharing the GPUs there are, e.g. two ranks on a one-GPU box.
+    backend = os.environ.get("QTX_BENCH_BACKEND", "nccl")
+    dev_index = local if backend == "nccl" else local % torch.cuda.device_count()
+    torch.cuda.set_device(dev_index)
+    coll_dev = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from qtx import _build
     if rank == 0:
@@ -296,7 +305,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], device="cuda")
+        t = torch.tensor([dt], device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     tokens = G * (L - 1) * args.steps
@@ -305,7 +314,7 @@ def main():
     # after the timed region: gather every rank's ids into global order and, on rank 0,
     # re-decode a sample of sentences from every shard in one batch of its own (per-token
     # quantization: a sentence's tokens do not depend on its batch)
-    allids = gather_ids(dist, ids, idx, G, world) if world > 1 else None
+    allids = gather_ids(dist, ids.to(coll_dev), idx, G, world) if world > 1 else None
     verified = None
     if rank == 0:
         if allids is None:
