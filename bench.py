@@ -118,10 +118,12 @@ def pmc_traffic():
         return json.load(f).get("traffic_bytes_per_launch")
 
 
-def time_row_gemms(M=256 * 128, reps=10):
+def time_row_gemms(M=256 * 128, reps=10, ws=True):
     """The five QuantLinear launches of one cfg3 encoder layer through qtx_linear_rows on
     synthetic int8 operands (QKV + per-token quant, O + residual + LN + quant, FFN1 row-max
-    pass, FFN1 ReLU + quant pass, FFN2 + residual + LN + quant): (us per launch, ops)."""
+    pass, FFN1 ReLU + quant pass, FFN2 + residual + LN + quant): (us per launch, ops).
+    ws: the Q/K/V and FFN1 launches on the weight-stationary kernel (kp = 2), as the encoder
+    runs them at this M (csrc/qtx_api.hip rowgemm); O and FFN2 on the KP row GEMM."""
     import ctypes as C
 
     import torch
@@ -143,10 +145,12 @@ def time_row_gemms(M=256 * 128, reps=10):
     pm = torch.full((4, M), 3.0, device="cuda")
     # the encoder runs the KP instances (csrc/qtx_api.hip encoder_run: kp = 1): weights
     # packed by qtx_pack_w_kp, A in the KP layout (random bytes: any layout of them is)
+    kps = {}
     for (N, K), w in list(W.items()):
         wk = torch.empty_like(w)
-        _lib.call("qtx_pack_w_kp", C.c_void_p(w.data_ptr()), N, K, C.c_void_p(wk.data_ptr()),
-                  C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        kps[(N, K)] = 2 if (ws and K == D and N != D) else 1   # Q/K/V and FFN1 (qtx_api.hip qws)
+        _lib.call("qtx_pack_w_ws" if kps[(N, K)] == 2 else "qtx_pack_w_kp", C.c_void_p(w.data_ptr()),
+                  N, K, C.c_void_p(wk.data_ptr()), C.c_void_p(torch.cuda.current_stream().cuda_stream))
         W[(N, K)] = wk
     cases = [("qkv_quant", 3 * D, D, a512, dict(epi=0, out8=out8, ldo8=D, o8_ts=M * D, os=os_, os_ts=M)),
              ("o_res_ln", D, D, a512, dict(epi=1, res=x, xout=x, ln_a=lna, ln_b=lnb, lnq=out8, lns=os_)),
@@ -157,7 +161,7 @@ def time_row_gemms(M=256 * 128, reps=10):
     res = {}
     for name, N, K, a, kw in cases:
         args = _lib.RowGemm()
-        for k, v in dict(A=a, sa=sa, W=W[(N, K)], sw=sw, bias=bias, M=M, N=N, K=K, kp=1, **kw).items():
+        for k, v in dict(A=a, sa=sa, W=W[(N, K)], sw=sw, bias=bias, M=M, N=N, K=K, kp=kps[(N, K)], **kw).items():
             setattr(args, k, v.data_ptr() if hasattr(v, "data_ptr") else v)
         for _ in range(3):
             _lib.call("qtx_linear_rows", C.byref(args), st)

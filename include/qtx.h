@@ -244,13 +244,23 @@ typedef struct qtx_row_gemm {
   /* kp = 1: A [M (+1 if odd), K] and W in the KP layout (row pair p, K chunk c of 64 bytes
    * = one 128-byte line at ((p * K/64 + c) * 128), rows 2p | 2p+1 at +0 | +64; W packed by
    * qtx_pack_w_kp); lnq (epi 1) and out8 (epi 3) are then written KP, epi 0's out8 row-major.
-   * K % 256 == 0. */
+   * K % 256 == 0.
+   * kp = 2: the weight-stationary kernel (K == 512 only): A in the KP layout, W packed by
+   * qtx_pack_w_ws; each workgroup keeps a 512-column slice of W on chip and streams 64-row
+   * blocks of A.  Outputs exactly as kp = 1, except that epi 3's out8 must hold M + (M & 1)
+   * rows (the KP pad row of an odd M is written as scratch). */
   int32_t kp;
 } qtx_row_gemm;
 int32_t qtx_linear_rows(const qtx_row_gemm* args, void* stream);
 /* W int8 [N, K] row-major -> out [N, K] in the KP layout with the per-512-column-tile row
  * order qtx_linear_rows(kp = 1) reads.  N % 512 == 0, K % 64 == 0. */
 int32_t qtx_pack_w_kp(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* stream);
+/* W int8 [N, 512] row-major -> out (N*512 bytes) in the order qtx_linear_rows(kp = 2) reads:
+ * for 512-column slice t, wave w (0..7), K step s (0..7), column fragment j (0..3) one 1 KB
+ * block at ((t*8 + w)*8 + s)*4 + j whose 16-byte lane l (0..63) holds
+ * W[512t + 64w + 16((l & 15) >> 2) + 4j + (l & 3)][64s + 16(l >> 4) .. +16].
+ * N % 512 == 0, K == 512. */
+int32_t qtx_pack_w_ws(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* stream);
 
 /* Skinny int8 GEMM for decode (M small): out = epilogue(A . W^T) with the A operand made
  * in the prologue: amode 0 = int8 A [M,K] + sa; 1 = LayerNorm(X [M,512]; ln_a, ln_b) then

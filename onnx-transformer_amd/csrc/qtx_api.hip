@@ -63,6 +63,7 @@ struct QLin {
   float* b = nullptr;
   int N = 0, K = 0;
   int8_t* qkp = nullptr;   // encoder, 8-bit: q in the row GEMM's KP layout (pack_w_kp)
+  int8_t* qws = nullptr;   // encoder, 8-bit, K == 512: q in the weight-stationary order
 };
 
 struct EncLayer {
@@ -229,6 +230,9 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     if (c.weight_bits == 8)      // KP copies for the encoder's row GEMMs
       for (auto& e : m->enc)
         for (QLin* L : {&e.qkv, &e.o, &e.w1, &e.w2}) L->qkp = ar.take<int8_t>((size_t)L->N * L->K);
+    if (c.weight_bits == 8 && c.d_ff % 512 == 0)   // weight-stationary copies (K = 512 GEMMs)
+      for (auto& e : m->enc)
+        for (QLin* L : {&e.qkv, &e.w1}) L->qws = ar.take<int8_t>((size_t)L->N * L->K);
     for (auto& d : m->dec) {
       lin(d.qkv, 3 * D, D); lin(d.o, D, D); lin(d.cq, D, D); lin(d.ckv, 2 * D, D);
       lin(d.co, D, D); lin(d.w1, F, D); lin(d.w2, D, F);
@@ -291,9 +295,10 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
   if (rc) { qtx_model_destroy(m); return rc; }
   for (auto& e : m->enc)
     for (QLin* L : {&e.qkv, &e.o, &e.w1, &e.w2})
-      if (L->qkp && launch_pack_w_kp(L->q, L->N, L->K, L->qkp, st) != hipSuccess) {
+      if ((L->qkp && launch_pack_w_kp(L->q, L->N, L->K, L->qkp, st) != hipSuccess) ||
+          (L->qws && launch_pack_w_ws(L->q, L->N, L->K, L->qws, st) != hipSuccess)) {
         qtx_model_destroy(m);
-        return fail(QTX_E_HIP, "KP weight pack");
+        return fail(QTX_E_HIP, "KP / WS weight pack");
       }
   // norms: order of weights.py:norm_names — enc L x 2, enc final, dec L x 3, dec final
   const int nb = norm_tensor_base(c);
@@ -506,13 +511,28 @@ bool row_path(const qtx_config& c) {
   return c.weight_bits == 8 && c.d_ff % 512 == 0 && !getenv("QTX_NO_ROWGEMM");
 }
 // kp: A (a8) in the KP layout and W from L.qkp; the int8 lnq / FFN-hidden outputs are
-// then written KP as well (RE_QUANT's q8 stays row-major: attention reads it)
+// then written KP as well (RE_QUANT's q8 stays row-major: attention reads it).
+// With kp, a K = 512 GEMM over many rows runs weight-stationary (kp = 2, W from L.qws):
+// each workgroup keeps a 512-column slice of W on chip (qtx_wsgemm.hip); below ws_min_m
+// rows the per-workgroup W load is not amortized and the row GEMM is faster.
+long ws_min_m() {
+  static const long v = [] {
+    const char* e = getenv("QTX_WS_MIN_M");
+    return e ? atol(e) : 8192L;
+  }();
+  return v;
+}
 RowGemmArgs rowgemm(const QLin& L, const int8_t* a8, const float* sa, int M, int epi,
                     bool kp = false) {
   RowGemmArgs g{};
-  g.A = a8; g.lda = L.K; g.sa = sa; g.W = kp ? L.qkp : L.q; g.ldw = L.K; g.sw = L.s; g.bias = L.b;
-  g.M = M; g.N = L.N; g.K = L.K; g.epi = epi; g.kp = kp;
+  const bool ws = kp && L.qws && L.K == 512 && M >= ws_min_m();
+  g.A = a8; g.lda = L.K; g.sa = sa; g.W = ws ? L.qws : kp ? L.qkp : L.q; g.ldw = L.K;
+  g.sw = L.s; g.bias = L.b;
+  g.M = M; g.N = L.N; g.K = L.K; g.epi = epi; g.kp = ws ? 2 : kp;
   return g;
+}
+hipError_t launch_row_gemm_any(const RowGemmArgs& g, hipStream_t st) {
+  return g.kp == 2 ? launch_gemm_ws(g, st) : launch_gemm_row(g, st);
 }
 // out = per-token quantized (a8 . W^T) per 512-wide tile into out8 + t*M*512, os + t*M
 int row_quant(const QLin& L, const int8_t* a8, const float* sa, int M, int8_t* out8,
@@ -520,7 +540,7 @@ int row_quant(const QLin& L, const int8_t* a8, const float* sa, int M, int8_t* o
   RowGemmArgs g = rowgemm(L, a8, sa, M, RE_QUANT, kp);
   g.fault = fa;
   g.out8 = out8; g.ldo8 = 512; g.o8_ts = (long)M * 512; g.os = os; g.os_ts = M;
-  HIPCHK(launch_gemm_row(g, st));
+  HIPCHK(launch_row_gemm_any(g, st));
   return QTX_OK;
 }
 // x += a8 . W^T, then LayerNorm(x) (ln) quantized into (lnq, lns) or fp32 into lnout
@@ -531,7 +551,7 @@ int row_res_ln(const QLin& L, const int8_t* a8, const float* sa, int M, float* x
   g.fault = fa;
   g.res = x; g.xout = x; g.ln_a = ln[0]; g.ln_b = ln[1];
   g.lnq = lnq; g.lns = lns; g.lnout = lnout;
-  HIPCHK(launch_gemm_row(g, st));
+  HIPCHK(launch_row_gemm_any(g, st));
   return QTX_OK;
 }
 // FFN1: relu(a8 . W1^T) quantized per token over all d_ff columns, two passes (row
@@ -542,11 +562,11 @@ int row_ffn1(const qtx_config& c, const QLin& L, const int8_t* a8, const float* 
   RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RELU_PMAX, kp);
   g.fault = fa;
   g.pmax_out = s.pmax;
-  HIPCHK(launch_gemm_row(g, st));
+  HIPCHK(launch_row_gemm_any(g, st));
   g.epi = RE_RELU_QUANT_PMAX;
   g.pmax_in = s.pmax; g.pmax_n = c.d_ff / 512;
   g.out8 = s.h8; g.ldo8 = c.d_ff; g.os = s.sh;
-  HIPCHK(launch_gemm_row(g, st));
+  HIPCHK(launch_row_gemm_any(g, st));
   return QTX_OK;
 }
 
@@ -1534,9 +1554,10 @@ int32_t qtx_linear_rows(const qtx_row_gemm* a, void* stream) {
                   (g.epi == RE_RELU_PMAX && g.pmax_out) ||
                   (g.epi == RE_RELU_QUANT_PMAX && g.out8 && g.os && g.pmax_in && g.pmax_n > 0);
   if (!ok) return fail(QTX_E_INVALID, "operands missing for epi %d", g.epi);
-  const hipError_t e = launch_gemm_row(g, (hipStream_t)stream);
+  const hipError_t e = g.kp == 2 ? launch_gemm_ws(g, (hipStream_t)stream)
+                                  : launch_gemm_row(g, (hipStream_t)stream);
   if (e == hipErrorInvalidValue)
-    return fail(QTX_E_UNSUPPORTED, "rows GEMM: N=%d K=%d epi=%d", g.N, g.K, g.epi);
+    return fail(QTX_E_UNSUPPORTED, "rows GEMM: N=%d K=%d epi=%d kp=%d", g.N, g.K, g.epi, g.kp);
   HIPCHK(e);
   return QTX_OK;
 }
@@ -1545,6 +1566,14 @@ int32_t qtx_pack_w_kp(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* 
   if (!W || !out) return fail(QTX_E_INVALID, "null argument");
   const hipError_t e = launch_pack_w_kp(W, N, K, out, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "pack_w_kp N=%d K=%d", N, K);
+  HIPCHK(e);
+  return QTX_OK;
+}
+
+int32_t qtx_pack_w_ws(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* stream) {
+  if (!W || !out) return fail(QTX_E_INVALID, "null argument");
+  const hipError_t e = launch_pack_w_ws(W, N, K, out, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "pack_w_ws N=%d K=%d", N, K);
   HIPCHK(e);
   return QTX_OK;
 }

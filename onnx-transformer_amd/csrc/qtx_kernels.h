@@ -146,6 +146,11 @@ struct RowGemmArgs {
 // tile (LDS row rho holds column (rho & ~127) + 8 (rho & 15) + ((rho >> 4) & 7))
 hipError_t launch_pack_w_kp(const int8_t* W, int N, int K, int8_t* out, hipStream_t st);
 hipError_t launch_gemm_row(const RowGemmArgs& a, hipStream_t st);
+// Weight-stationary variant for K == 512 (qtx_wsgemm.hip): each workgroup keeps a 512-column
+// slice of W in registers and streams 64-row blocks of A (KP layout); W packed by
+// launch_pack_w_ws.  Same epilogues and outputs as launch_gemm_row(kp = 1); no faults.
+hipError_t launch_gemm_ws(const RowGemmArgs& a, hipStream_t st);
+hipError_t launch_pack_w_ws(const int8_t* W, int N, int K, int8_t* out, hipStream_t st);
 
 hipError_t launch_gemm(const GemmArgs& a, int wbits, hipStream_t st);
 hipError_t launch_skinny(const SkinnyArgs& a, int wbits, hipStream_t st);

@@ -1,0 +1,714 @@
+// qtx_wsgemm.hip — the encoder's K = 512 QuantLinear GEMMs, weight-stationary
+// (quant_linear.py:111-119; Q/K/V, O-projection and FFN1 of encoder.py at large M):
+//   out[m, n] = epilogue( sum_k A[m,k] * W[n,k] ),  y = ((float(acc) * sa[m]) * sw[n]) + b[n]
+//
+// Why: k_gemm_row streams BOTH operands through LDS (128 x 512 tile, 205 int8 ops per LDS
+// byte) and is bound by the ~70 GB/s per-CU L2 -> LDS fill.  At K = 512 a whole 512-column
+// slice of W is 256 KB — half of a CU's 512 KB register file.  So each workgroup keeps its
+// slice of W on chip for the whole launch (wave w: columns 64w..64w+63, K steps 0-4 in 80
+// VGPRs and K steps 5-7 in LDS: with 2 waves per SIMD a wave has 256 registers, and the
+// accumulators and epilogues need the rest), and only A moves: 64-row blocks (32 KB) by
+// LDS-DMA, read by all 8 waves — 512 ops per LDS byte filled, so the MFMA pipe, not the
+// fill, paces the main loop.  The workgroup is persistent over the row blocks of its slice.
+//
+// The MFMA computes the transposed tile C^T = W . A^T (W fragments as the A operand): its
+// output layout then gives each lane 4 token rows (16i + (lane & 15)) x 16 CONSECUTIVE
+// output columns — 4 per-row scalars per lane instead of 16, one 16-byte int8 store per row,
+// and a row's partial max over the wave's 64 columns in 2 cross-lane steps.
+//
+// Layouts (all K = 512):
+//   A   KP layout (qtx_common.h kp_off), as the encoder's producers write it.
+//   W   "WS" layout (k_pack_w_ws): for slice t, wave w, K step s (64 B), fragment j, 1 KB in
+//       MFMA operand lane order: lane l holds W[n][64s + 16(l>>4) .. +16] with
+//       n = 512t + 64w + 16((l & 15) >> 2) + 4j + (l & 3), so that C^T row 4q + e of
+//       fragment j (lane group q = l >> 4, element e) is column 512t + 64w + 16q + 4j + e.
+//   LDS A tile: piece (s, i) = row fragment i (16 rows), K step s: 1 KB in MFMA lane order
+//       (lane l: row 16i + (l & 15), bytes 64s + 16(l>>4)) — conflict-free lane-linear
+//       ds_read_b128; filled from KP lines (8 full 128-byte lines per piece).
+// Epilogues (RowEpi, qtx_kernels.h): RE_QUANT (per-token quant over the 512-column slice),
+// RE_RES_LN (N = 512: residual + next LayerNorm + quant), RE_RELU_PMAX, RE_RELU_QUANT_PMAX.
+// Numerics: identical to k_gemm_row (the same canonical order; GPU == oracle bit for bit).
+#include "qtx_common.h"
+#include "qtx_kernels.h"
+
+#include <cstdlib>
+
+QTX_STAMP_SETTER(ws)
+
+namespace {
+bool getenv_flag(const char* name) {        // experiment switches (A/B on one box)
+  const char* v = getenv(name);
+  return v && *v && *v != '0';
+}
+}  // namespace
+
+namespace qtx {
+
+constexpr int WS_K = 512, WS_R = 64;
+constexpr int WS_STAGE = WS_R * WS_K;          // 32 KB: one A row block in fragment order
+constexpr int WS_SR = 5;                        // K steps of W held in registers (rest: LDS)
+constexpr int WS_WL = 8 * (8 - WS_SR) * 4 * 1024;   // W's LDS part: 96 KB
+
+// Raw buffer stores with the hardware range check (a store at or past `bytes` is dropped):
+// the epilogue's stores are then unconditional, so every wave issues the same known number
+// of them and the next block's top can wait with a counted vmcnt instead of draining them.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ws_rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
+                                           0x00020000);
+}
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+template <int EPI>
+__global__ __launch_bounds__(512) void k_gemm_ws(RowGemmArgs g) {
+  // LDS (160 KB): A stages | W K steps 5-7 (96 KB) | epilogue staging.  RES_LN keeps ONE A
+  // stage (the next block's DMA flies under the epilogue) and stages y a quarter block (16
+  // rows, 32 KB) at a time; the others keep two A stages (the next block's DMA flies under
+  // this block's MFMAs) and exchange partial row maxima in the consumed stage.
+  constexpr int NST = EPI == RE_RES_LN ? 1 : 2;
+  constexpr int EXTRA = EPI == RE_RES_LN ? 16 * 512 * 4 : 0;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NST * WS_STAGE + WS_WL + EXTRA];
+  uint8_t* const wl = lds + NST * WS_STAGE;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int f = lane & 15, gq = lane >> 4;
+  const int nsl = g.N >> 9;
+  const int wpt = gridDim.x / nsl;               // workgroups per slice
+  const int t = blockIdx.x % nsl, r0 = blockIdx.x / nsl;
+  const int nb = (g.M + WS_R - 1) / WS_R;
+  if (r0 >= nb) return;
+  QTX_STAMP(0);
+
+  auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  // wave w moves K step w of the four row fragments (4 pieces of 8 KP lines)
+  auto issue = [&](uint8_t* st, int rb) {
+    const int m0 = rb * WS_R;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long row = min(m0 + 16 * i + f, g.M - 1);
+      dma16(g.A + kp_off(row, 64 * wave + 16 * gq, WS_K), st + ((wave * 4 + i) << 10));
+    }
+  };
+  issue(lds, r0);
+
+  // this wave's W fragments, resident for the whole launch: K steps 5-7 into LDS (12
+  // pieces, DMA), 0-4 into registers (K-step order: the first MFMAs wait only for the first
+  // loads)
+  v4i wr[WS_SR][4];
+  {
+    const int8_t* wsrc = g.W + ((long)(t * 8 + wave) << 15);
+#pragma unroll
+    for (int p = 0; p < (8 - WS_SR) * 4; ++p)
+      dma16(wsrc + ((WS_SR * 4 + p) << 10) + lane * 16, wl + ((wave * (8 - WS_SR) * 4 + p) << 10));
+    const v4i* ws = reinterpret_cast<const v4i*>(wsrc) + lane;
+#pragma unroll
+    for (int s = 0; s < WS_SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wr[s][j] = ws[(s * 4 + j) * 64];
+    // consume them here: otherwise the compiler's wait for them lands at the top of the
+    // block loop, where vmcnt(0) would also wait for the next block's DMA every iteration
+#pragma unroll
+    for (int s = 0; s < WS_SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(wr[s][j]));
+  }
+  const int cs = 64 * wave + 16 * gq;            // the lane's 16 columns within the slice
+  const int c0 = 512 * t + cs;                   // ... within the whole output row
+
+  int it = 0;
+  for (int rb = r0; rb < nb; rb += wpt, ++it) {
+    const int m0 = rb * WS_R;
+    uint8_t* cur = lds + (NST == 2 ? (it & 1) * WS_STAGE : 0);
+    // this wave's DMA of the block retired (only the previous epilogue's unconditional
+    // stores, issued after it, may still be in flight: vmcnt retires in issue order); the
+    // barrier makes every wave's part visible and frees the other stage / the epilogue areas
+    if constexpr (EPI == RE_QUANT) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if constexpr (EPI == RE_RELU_QUANT_PMAX) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (EPI == RE_RELU_PMAX) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (it == 0) QTX_STAMP(1);
+    // per-row operands of the block, one row per lane (fetched by ds_bpermute later); issued
+    // BEFORE the next block's DMA: vmcnt retires in issue order, so waiting for these loads
+    // does not wait for the DMA
+    const int lrow = min(m0 + lane, g.M - 1);
+    const float sa_l = g.sa[lrow];
+    float pmv[4] = {0.0f, 0.0f, 0.0f, 0.0f};     // reduced in the epilogue, not here
+    if constexpr (EPI == RE_RELU_QUANT_PMAX) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) pmv[p] = g.pmax_in[(long)min(p, g.pmax_n - 1) * g.M + lrow];
+    }
+    if (NST == 2 && rb + wpt < nb) issue(lds + ((it + 1) & 1) * WS_STAGE, rb + wpt);
+
+    // acc[i][j]: C^T fragment (W fragment j) x (token row fragment i)
+    v4i acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+    // sw / bias of the lane's 16 columns: issued during the last K steps (scheduling
+    // barriers keep them there and keep their consumers out of the main loop: a compiler wait
+    // inside the loop would also wait for the next block's DMA, vmcnt retiring in order)
+    float4 sw4[4], b4[4];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (s == 6) {
+        __builtin_amdgcn_sched_barrier(0);
+        const float4* swp = reinterpret_cast<const float4*>(g.sw + c0);
+        const float4* bp = reinterpret_cast<const float4*>(g.bias + c0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { sw4[j] = swp[j]; b4[j] = bp[j]; }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      v4i a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = *reinterpret_cast<const v4i*>(cur + ((s * 4 + i) << 10) + lane * 16);
+      v4i b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = s < WS_SR ? wr[s < WS_SR ? s : 0][j]
+                         : *reinterpret_cast<const v4i*>(wl + (((wave * (8 - WS_SR) + s - WS_SR) * 4 + j) << 10) + lane * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#ifdef QTX_WS_NOMFMA                               // diagnostic builds only
+          asm volatile("" ::"v"(a[i]), "v"(b[j]));
+#else
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+#endif
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (it < 5) QTX_STAMP(2 + 2 * it);
+#ifdef QTX_WS_NOEPI                                 // diagnostic builds only: main loop alone
+    {
+      int sum = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+      if (sum == 0x7fffffff) g.out8[0] = (int8_t)(sw4[0].x + b4[0].x);
+      continue;
+    }
+#endif
+    if constexpr (NST == 1) {
+      // every wave is past its fragment reads: the stage takes the next block's DMA now
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (rb + wpt < nb) issue(lds, rb + wpt);
+    }
+
+    // ---- y = ((float(acc) * sa[m]) * sw[n]) + b[n]; lane: token rows 16i + f, columns
+    // cs + 4j + e (16 consecutive: y[i][4j + e])
+    float y[4][16];
+    {
+      // opaque: keeps the compiler from hoisting the consumers of the per-row loads (and
+      // with them a vmcnt wait that would include the next block's DMA) into the main loop
+      float sa_e = sa_l;
+      asm volatile("" : "+v"(sa_e));
+      float sr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        sr[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sa_e)));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float swj[4] = {sw4[j].x, sw4[j].y, sw4[j].z, sw4[j].w};
+        const float bj[4] = {b4[j].x, b4[j].y, b4[j].z, b4[j].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = ((float)acc[i][j][e] * sr[i]) * swj[e] + bj[e];
+            // relu: v > 0 ? v : 0 up to the sign of a zero, which no consumer sees (the
+            // row max takes |.|, the quantizer maps +-0 to the same code)
+            y[i][4 * j + e] = (EPI == RE_RELU_PMAX || EPI == RE_RELU_QUANT_PMAX) ? fmaxf(v, 0.0f) : v;
+          }
+      }
+    }
+
+    if (it == 0) QTX_STAMP(12);
+    if constexpr (EPI == RE_RES_LN) {
+      // four quarters of 16 rows (row fragment qq): stage y as fp32 rows [16][512] (16-byte
+      // chunk c of row r at chunk position c ^ (r & 7): conflict-free writes and reads);
+      // wave w then takes rows 2w, 2w+1 of the quarter: x = res + y (residual in the
+      // canonical lane layout, loaded before the staging), x out, LayerNorm (ln_rows512),
+      // per-token quant (or fp32 out)
+      float* stg = reinterpret_cast<float*>(wl + WS_WL);
+      float ga[2][4], gb[2][4];
+      ln_params512(g.ln_a, g.ln_b, lane, ga, gb);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int rowb = m0 + 16 * qq + 2 * wave;
+        float4 rv[2][2];
+#pragma unroll
+        for (int r2 = 0; r2 < 2; ++r2) {
+          const int row = min(rowb + r2, g.M - 1);
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            rv[r2][c] = *reinterpret_cast<const float4*>(g.res + (long)row * 512 + 4 * (lane + 64 * c));
+        }
+        if (qq > 0) {                             // every wave is done reading the last quarter
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<float4*>(stg + f * 512 + 4 * ((cs / 4 + j) ^ (f & 7))) =
+              make_float4(y[qq][4 * j], y[qq][4 * j + 1], y[qq][4 * j + 2], y[qq][4 * j + 3]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        float v[2][2][4];
+#pragma unroll
+        for (int r2 = 0; r2 < 2; ++r2)
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int r = 2 * wave + r2;
+            const float4 t4 = *reinterpret_cast<const float4*>(stg + r * 512 + 4 * ((lane + 64 * c) ^ (r & 7)));
+            v[r2][c][0] = rv[r2][c].x + t4.x; v[r2][c][1] = rv[r2][c].y + t4.y;
+            v[r2][c][2] = rv[r2][c].z + t4.z; v[r2][c][3] = rv[r2][c].w + t4.w;
+          }
+#pragma unroll
+        for (int r2 = 0; r2 < 2; ++r2)
+          if (rowb + r2 < g.M)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+              *reinterpret_cast<float4*>(g.xout + (long)(rowb + r2) * 512 + 4 * (lane + 64 * c)) =
+                  make_float4(v[r2][c][0], v[r2][c][1], v[r2][c][2], v[r2][c][3]);
+        ln_rows512<2>(v, ga, gb);
+        if (g.lnq) {
+          uint32_t qd[2][2];
+          float sc[2];
+          quant_rows512<2>(v, qd, sc);
+#pragma unroll
+          for (int r2 = 0; r2 < 2; ++r2)
+            if (rowb + r2 < g.M) {
+              const long row = rowb + r2;
+              *reinterpret_cast<uint32_t*>(g.lnq + kp_off(row, 4 * lane, 512)) = qd[r2][0];
+              *reinterpret_cast<uint32_t*>(g.lnq + kp_off(row, 4 * (lane + 64), 512)) = qd[r2][1];
+              if (lane == 0) g.lns[row] = sc[r2];
+            }
+        } else {
+#pragma unroll
+          for (int r2 = 0; r2 < 2; ++r2)
+            if (rowb + r2 < g.M)
+#pragma unroll
+              for (int c = 0; c < 2; ++c)
+                *reinterpret_cast<float4*>(g.lnout + (long)(rowb + r2) * 512 + 4 * (lane + 64 * c)) =
+                    make_float4(v[r2][c][0], v[r2][c][1], v[r2][c][2], v[r2][c][3]);
+        }
+      }
+      if (it < 5) QTX_STAMP(3 + 2 * it);
+      continue;
+    } else {
+      // ---- the row's absmax over the 512-column slice (QUANT, RELU_PMAX: the wave's 64
+      // columns in 16 values x the 4 lane groups, then the 8 waves through LDS) or over the
+      // whole row from the partial maxima (RELU_QUANT_PMAX); one row per lane after that
+      float m;
+      if constexpr (EPI == RE_RELU_QUANT_PMAX) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) asm volatile("" : "+v"(pmv[p]));
+        m = fmaxf(fmaxf(pmv[0], pmv[1]), fmaxf(pmv[2], pmv[3]));
+        for (int p = 4; p < g.pmax_n; ++p) m = fmaxf(m, g.pmax_in[(long)p * g.M + lrow]);
+      } else {
+        float pm[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float a = fabsf(y[i][0]);
+#pragma unroll
+          for (int c = 1; c < 16; ++c) a = fmaxf(a, fabsf(y[i][c]));
+          a = fmaxf(a, __shfl_xor(a, 16));
+          pm[i] = fmaxf(a, __shfl_xor(a, 32));
+        }
+        // the block's A stage is free once every wave is past its fragment reads: it holds
+        // the per-wave partial maxima [8][64]
+        float* red = reinterpret_cast<float*>(cur);
+        if (it == 0) QTX_STAMP(13);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (it == 0) QTX_STAMP(14);
+        if (gq == 0)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) red[wave * WS_R + 16 * i + f] = pm[i];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        m = red[lane];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w * WS_R + lane]);
+        if (it == 0) QTX_STAMP(15);
+      }
+      const int orow = m0 + lane;
+      if constexpr (EPI == RE_RELU_PMAX) {
+        // every wave stores the (identical) row maxima: 1 store per wave (counted above)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m), ws_rsrc(g.pmax_out + (long)t * g.M, 4L * g.M),
+                                              4 * orow, 0, 0);
+        if (it < 5) QTX_STAMP(3 + 2 * it);
+        continue;
+      } else {
+        // per-token quantization rint(y / s) with the correctly rounded quotient (div_cr:
+        // shared reciprocal per row), guard as in k_gemm_row: rmax < 2^37 for every row of
+        // the block, else every lane takes the true division (uniform branch)
+        const float sc_l = quant_scale(m, 127.0f);
+        const float inv_l = 1.0f / sc_l;
+        const bool big = __ballot(!(m < 0x1p37f)) != 0ull;
+        // every wave stores the (identical) scales: 1 store per wave (RELU_QUANT_PMAX: in the
+        // slice-0 workgroups only, so the counted wait there does not include it)
+        if (EPI == RE_QUANT || t == 0)
+          __builtin_amdgcn_raw_buffer_store_b32(
+              __float_as_uint(sc_l), ws_rsrc(EPI == RE_QUANT ? g.os + (long)t * g.os_ts : g.os, 4L * g.M),
+              4 * orow, 0, 0);
+        float sc[4], inv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sc[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sc_l)));
+          inv[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(inv_l)));
+        }
+        // data: 4 x 16 bytes per lane, unconditional (rows >= M fall past the range; the KP
+        // output's range includes the pad row of an odd M, which is scratch)
+        const __amdgpu_buffer_rsrc_t orsrc =
+            EPI == RE_QUANT ? ws_rsrc(g.out8 + (long)t * g.o8_ts, (long)g.M * g.ldo8)
+                            : ws_rsrc(g.out8, (long)(g.M + (g.M & 1)) * g.ldo8);
+        auto store = [&](auto quot) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            uint32_t d[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              d[j] = pack4_biased(rint_biased(quot(y[i][4 * j], sc[i], inv[i])),
+                                  rint_biased(quot(y[i][4 * j + 1], sc[i], inv[i])),
+                                  rint_biased(quot(y[i][4 * j + 2], sc[i], inv[i])),
+                                  rint_biased(quot(y[i][4 * j + 3], sc[i], inv[i])));
+            const long row = m0 + 16 * i + f;
+            const long off = EPI == RE_QUANT ? row * g.ldo8 + cs : kp_off(row, c0, g.ldo8);
+            __builtin_amdgcn_raw_buffer_store_b128(v4u{d[0], d[1], d[2], d[3]}, orsrc, (int)off, 0, 0);
+          }
+        };
+        if (__builtin_expect(big, 0))
+          store([](float a, float b, float) { return a / b; });
+        else
+          store([](float a, float b, float yy) { return div_cr(a, b, yy); });
+        if (it < 5) QTX_STAMP(3 + 2 * it);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing DMA (never read) drained
+}
+
+// =====================================================================================
+// k_gemm_wsp: the same weight-stationary GEMM, software-pipelined (RE_QUANT, RE_RELU_PMAX,
+// RE_RELU_QUANT_PMAX).  Measured on k_gemm_ws: the main loop alone runs at the MFMA floor
+// and the epilogue alone takes about as long again, and the two do not overlap (every wave
+// reaches its epilogue together).  Here row blocks are 32 rows and iteration b issues the
+// MFMAs of block b in the same basic blocks as the epilogue of block b-1 (y, row maxima,
+// quantization, stores), so the VALU / LDS latency chains of one block run under the
+// matrix work of the next.  Two barriers per block: the top one (block b's A landed in
+// every wave's part; the other stage and the max-exchange area free) and one between the
+// epilogue's two halves (the partial row maxima of block b-1 visible).
+// Nothing in an iteration waits for the next block's DMA: the only vector-memory loads of
+// an iteration (per-row scales / maxima of block b) are issued before it, sw / bias live in
+// LDS, and the stores are unconditional buffer stores, so the top of the next iteration
+// waits with a counted vmcnt.
+// =====================================================================================
+constexpr int WP_R = 32, WP_STAGE = WP_R * WS_K;    // 16 KB A stage
+// s_waitcnt immediates (gfx9 encoding: vmcnt bits 3:0 and 15:14, expcnt 6:4, lgkmcnt 11:8)
+constexpr int WAIT_VM(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70 | 0xF00; }
+constexpr int WAIT_LGKM0 = 0xC07F;
+
+template <int EPI>
+__global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
+  // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias of the slice (4 KB) |
+  // partial row maxima [8][32] (1 KB)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WS_WL + 4096 + 8 * WP_R * 4];
+  uint8_t* const wl = lds + 2 * WP_STAGE;
+  float* const swl = reinterpret_cast<float*>(wl + WS_WL);    // [512] sw, then [512] bias
+  float* const red = swl + 1024;                               // [8][32]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int f = lane & 15, gq = lane >> 4;
+  const int nsl = g.N >> 9;
+  const int wpt = gridDim.x / nsl;
+  const int t = blockIdx.x % nsl, r0 = blockIdx.x / nsl;
+  const int nb = (g.M + WP_R - 1) / WP_R;
+  if (r0 >= nb) return;
+  const int nblk = (nb - r0 + wpt - 1) / wpt;          // row blocks r0, r0 + wpt, ...
+
+  auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  // block k of this workgroup (clamped: past the last one the last is re-loaded, never read,
+  // so every iteration issues the same DMAs); wave w moves K step w of the 2 row fragments
+  auto issue = [&](int k) {
+    const int rb = r0 + min(k, nblk - 1) * wpt;
+    uint8_t* st = lds + (k & 1) * WP_STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long row = min(rb * WP_R + 16 * i + f, g.M - 1);
+      dma16(g.A + kp_off(row, 64 * wave + 16 * gq, WS_K), st + ((wave * 2 + i) << 10));
+    }
+  };
+  issue(0);
+  v4i wr[WS_SR][4];
+  {
+    const int8_t* wsrc = g.W + ((long)(t * 8 + wave) << 15);
+#pragma unroll
+    for (int p = 0; p < (8 - WS_SR) * 4; ++p)
+      dma16(wsrc + ((WS_SR * 4 + p) << 10) + lane * 16, wl + ((wave * (8 - WS_SR) * 4 + p) << 10));
+    const v4i* ws = reinterpret_cast<const v4i*>(wsrc) + lane;
+#pragma unroll
+    for (int s = 0; s < WS_SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wr[s][j] = ws[(s * 4 + j) * 64];
+    // sw / bias of the slice into LDS (wave w: 128 floats)
+    if (wave < 4) {
+      const int c = 128 * wave + 2 * lane;
+      *reinterpret_cast<float2*>(swl + c) = *reinterpret_cast<const float2*>(g.sw + 512 * t + c);
+      *reinterpret_cast<float2*>(swl + 512 + c) = *reinterpret_cast<const float2*>(g.bias + 512 * t + c);
+    }
+#pragma unroll
+    for (int s = 0; s < WS_SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(wr[s][j]));
+  }
+  const int cs = 64 * wave + 16 * gq;            // the lane's 16 columns within the slice
+  const int c0 = 512 * t + cs;
+  // outputs: unconditional range-checked buffer stores (rows >= M dropped)
+  const __amdgpu_buffer_rsrc_t orsrc =
+      EPI == RE_QUANT ? ws_rsrc(g.out8 + (long)t * g.o8_ts, (long)g.M * g.ldo8)
+                      : ws_rsrc(g.out8, EPI == RE_RELU_QUANT_PMAX ? (long)(g.M + (g.M & 1)) * g.ldo8 : 0L);
+  const __amdgpu_buffer_rsrc_t srsrc =
+      EPI == RE_RELU_PMAX ? ws_rsrc(g.pmax_out + (long)t * g.M, 4L * g.M)
+      : EPI == RE_QUANT   ? ws_rsrc(g.os + (long)t * g.os_ts, 4L * g.M)
+                          : ws_rsrc(g.os, t == 0 ? 4L * g.M : 0L);   // the slice-0 WGs store it
+
+  // per-row operands of block k: lane l holds row (l & 31) (loaded before the block's DMA)
+  auto rowops = [&](int k, float& sa, float (&pm)[4]) {
+    const int row = min(r0 * WP_R + min(k, nblk - 1) * wpt * WP_R + (lane & 31), g.M - 1);
+    sa = g.sa[row];
+    if constexpr (EPI == RE_RELU_QUANT_PMAX) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) pm[p] = g.pmax_in[(long)min(p, g.pmax_n - 1) * g.M + row];
+    }
+  };
+  auto mfma_steps = [&](v4i (&acc)[2][4], const uint8_t* cur, int s0, int s1) {
+#pragma unroll
+    for (int s = s0; s < s1; ++s) {
+      v4i a[2], b[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const v4i*>(cur + ((s * 2 + i) << 10) + lane * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = s < WS_SR ? wr[s < WS_SR ? s : 0][j]
+                         : *reinterpret_cast<const v4i*>(wl + (((wave * (8 - WS_SR) + s - WS_SR) * 4 + j) << 10) + lane * 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+    }
+  };
+  // epilogue of block k, first half: y (lane: rows 16i + f, columns cs .. cs+15) and, for
+  // QUANT / RELU_PMAX, the wave's partial row maxima into red
+  auto epi1 = [&](const v4i (&acc)[2][4], float sa, float (&y)[2][16]) {
+    float sr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      sr[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sa)));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 s4 = *reinterpret_cast<const float4*>(swl + cs + 4 * j);
+      const float4 b4 = *reinterpret_cast<const float4*>(swl + 512 + cs + 4 * j);
+      const float swj[4] = {s4.x, s4.y, s4.z, s4.w}, bj[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = ((float)acc[i][j][e] * sr[i]) * swj[e] + bj[e];
+          y[i][4 * j + e] = EPI == RE_QUANT ? v : fmaxf(v, 0.0f);   // relu up to the sign of 0
+        }
+    }
+    if constexpr (EPI != RE_RELU_QUANT_PMAX) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float a = fabsf(y[i][0]);
+#pragma unroll
+        for (int c = 1; c < 16; ++c) a = fmaxf(a, fabsf(y[i][c]));
+        a = fmaxf(a, __shfl_xor(a, 16));
+        a = fmaxf(a, __shfl_xor(a, 32));
+        red[wave * WP_R + 16 * i + f] = a;      // the 4 lane groups store the same value
+      }
+    }
+  };
+  // second half: the row max (8 waves' partials, or the FFN1 partial maxima), the scale,
+  // and the unconditional stores of block k
+  auto epi2 = [&](int k, const float (&y)[2][16], const float (&pm)[4]) {
+    const int m0 = (r0 + min(k, nblk - 1) * wpt) * WP_R;
+    float m;
+    if constexpr (EPI == RE_RELU_QUANT_PMAX) {
+      m = fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3]));   // pmax_n <= 4 (launch check)
+    } else {
+      m = red[lane & 31];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w * WP_R + (lane & 31)]);
+    }
+    // rows m0 + (lane & 31); lanes 32-63 duplicate 0-31 and store the same values
+    if constexpr (EPI == RE_RELU_PMAX) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m), srsrc, 4 * (m0 + (lane & 31)), 0, 0);
+    } else {
+      // rint(y / s) exactly: div_cr (shared reciprocal per row) on y and s both scaled by
+      // 2^-64 when the row max is >= 2^37 (an exact power-of-two scaling that keeps every
+      // intermediate of the Markstein step normal; |y / s| <= 127 either way) — branch-free
+      const float sc = quant_scale(m, 127.0f);
+      const float kk = m < 0x1p37f ? 1.0f : 0x1p-64f;
+      const float scs = sc * kk, invs = 1.0f / scs;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc), srsrc, 4 * (m0 + (lane & 31)), 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int src = 4 * (16 * i + f);
+        const float b = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(scs)));
+        const float yi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(invs)));
+        const float k2 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(kk)));
+        uint32_t d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          d[j] = pack4_biased(rint_biased(div_cr(y[i][4 * j] * k2, b, yi)),
+                              rint_biased(div_cr(y[i][4 * j + 1] * k2, b, yi)),
+                              rint_biased(div_cr(y[i][4 * j + 2] * k2, b, yi)),
+                              rint_biased(div_cr(y[i][4 * j + 3] * k2, b, yi)));
+        const long row = m0 + 16 * i + f;
+        const long off = EPI == RE_QUANT ? row * g.ldo8 + cs : kp_off(row, c0, g.ldo8);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{d[0], d[1], d[2], d[3]}, orsrc, (int)off, 0, 0);
+      }
+    }
+  };
+  auto top_wait = [&]() {
+    // the block's DMA retired (only the previous epilogue's stores — 3 per wave for the
+    // quantizing epilogues (2 rows of 16 bytes + the scale), 1 for RELU_PMAX — may still
+    // fly), then every wave's part visible (compiler-visible waits: its own wait insertion
+    // then knows what they retired)
+    if constexpr (EPI == RE_RELU_PMAX) __builtin_amdgcn_s_waitcnt(WAIT_VM(1));
+    else __builtin_amdgcn_s_waitcnt(WAIT_VM(3));
+    __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+    __builtin_amdgcn_s_barrier();
+  };
+  auto zero = [](v4i (&acc)[2][4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+  };
+
+  // ---- block 0: main loop only
+  v4i accp[2][4];
+  float sap, pmp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
+  __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+  __builtin_amdgcn_s_barrier();
+  rowops(0, sap, pmp);
+  issue(1);
+  zero(accp);
+  mfma_steps(accp, lds, 0, 8);
+  __builtin_amdgcn_s_waitcnt(WAIT_VM(0));   // block 1's DMA (no stores behind it yet)
+  // ---- steady state: block k's MFMAs with block k-1's epilogue
+  for (int k = 1; k < nblk; ++k) {
+    top_wait();
+    // last iteration's per-row loads complete HERE, before this iteration's loads and DMA:
+    // the compiler's wait for them at their use would otherwise count only its own younger
+    // loads and also wait for the DMA issued in between
+    asm volatile("" ::"v"(sap));
+#pragma unroll
+    for (int p = 0; p < 4; ++p) asm volatile("" ::"v"(pmp[p]));
+    float sac, pmc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    rowops(k, sac, pmc);
+    issue(k + 1);
+    const uint8_t* cur = lds + (k & 1) * WP_STAGE;
+    v4i acc[2][4];
+    zero(acc);
+    float y[2][16];
+    mfma_steps(acc, cur, 0, 4);
+    epi1(accp, sap, y);
+    __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+    __builtin_amdgcn_s_barrier();
+    mfma_steps(acc, cur, 4, 8);
+    epi2(k - 1, y, pmp);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) accp[i][j] = acc[i][j];
+    sap = sac;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) pmp[p] = pmc[p];
+  }
+  // ---- the last block's epilogue
+  {
+    top_wait();
+    float y[2][16];
+    epi1(accp, sap, y);
+    __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+    __builtin_amdgcn_s_barrier();
+    epi2(nblk - 1, y, pmp);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {
+  if (g.M <= 0) return hipSuccess;
+  if (g.K != WS_K || g.N % 512 || g.N <= 0 || (g.epi == RE_RES_LN && g.N != 512) ||
+      g.fault.kind != FK_NONE || (g.epi == RE_RELU_QUANT_PMAX && g.pmax_n <= 0))
+    return hipErrorInvalidValue;
+  const int nsl = g.N / 512;
+  if (g.epi != RE_RES_LN && g.pmax_n <= 4 && !getenv_flag("QTX_WS_NOPIPE")) {   // pipelined
+    const int nb = (g.M + WP_R - 1) / WP_R;
+    int wpt = 256 / nsl;
+    if (wpt > nb) wpt = nb;
+    const dim3 grid(nsl * wpt), block(512);
+    switch (g.epi) {
+      case RE_QUANT: k_gemm_wsp<RE_QUANT><<<grid, block, 0, st>>>(g); break;
+      case RE_RELU_PMAX: k_gemm_wsp<RE_RELU_PMAX><<<grid, block, 0, st>>>(g); break;
+      default: k_gemm_wsp<RE_RELU_QUANT_PMAX><<<grid, block, 0, st>>>(g); break;
+    }
+    return hipGetLastError();
+  }
+  const int nb = (g.M + WS_R - 1) / WS_R;
+  int wpt = 256 / nsl;
+  if (wpt > nb) wpt = nb;
+  if (wpt < 1) wpt = 1;
+  const dim3 grid(nsl * wpt), block(512);
+  switch (g.epi) {
+    case RE_QUANT: k_gemm_ws<RE_QUANT><<<grid, block, 0, st>>>(g); break;
+    case RE_RES_LN: k_gemm_ws<RE_RES_LN><<<grid, block, 0, st>>>(g); break;
+    case RE_RELU_PMAX: k_gemm_ws<RE_RELU_PMAX><<<grid, block, 0, st>>>(g); break;
+    case RE_RELU_QUANT_PMAX: k_gemm_ws<RE_RELU_QUANT_PMAX><<<grid, block, 0, st>>>(g); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// W [N, 512] row-major -> the WS layout (header): one thread per 16-byte chunk.
+__global__ void k_pack_w_ws(const int8_t* W, int N, int8_t* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;   // output chunk index
+  if (i >= (long)N * 32) return;
+  const int lane = (int)(i & 63), j = (int)((i >> 6) & 3), s = (int)((i >> 8) & 7);
+  const int w = (int)((i >> 11) & 7), t = (int)(i >> 14);
+  const int r = lane & 15;
+  const long n = 512L * t + 64 * w + 16 * (r >> 2) + 4 * j + (r & 3);
+  *reinterpret_cast<uint4*>(out + 16 * i) =
+      *reinterpret_cast<const uint4*>(W + n * WS_K + 64 * s + 16 * (lane >> 4));
+}
+
+hipError_t launch_pack_w_ws(const int8_t* W, int N, int K, int8_t* out, hipStream_t st) {
+  if (N % 512 || N <= 0 || K != WS_K) return hipErrorInvalidValue;
+  const long nch = (long)N * 32;
+  k_pack_w_ws<<<dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, st>>>(W, N, out);
+  return hipGetLastError();
+}
+
+}  // namespace qtx

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 REPO = os.path.dirname(os.path.dirname(HERE))
 LIB = os.path.join(HERE, "libqtx.so")
-SOURCES = ["qtx_kernels.hip", "qtx_decode.hip", "qtx_gemm.hip", "qtx_attn.hip", "qtx_api.hip"]
+SOURCES = ["qtx_kernels.hip", "qtx_decode.hip", "qtx_gemm.hip", "qtx_wsgemm.hip", "qtx_attn.hip", "qtx_api.hip"]
 HEADERS = ["qtx_common.h", "qtx_kernels.h"]
 
 # -ffp-contract=off: every float op is a separate IEEE op (the numerics contract,

@@ -77,6 +77,7 @@ SIGNATURES = {
     "qtx_linear_i8": (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, P, P, P]),
     "qtx_linear_rows": (I32, [C.POINTER(RowGemm), P]),
     "qtx_pack_w_kp": (I32, [P, I32, I32, P, P]),
+    "qtx_pack_w_ws": (I32, [P, I32, I32, P, P]),
     "qtx_pack_int4": (I32, [P, I32, I32, P, P]),
     "qtx_attention_i8": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, P]),
     "qtx_attention_i8_quant": (I32, [P, P, P, P, P, P, P, I32, I32, P, P, P]),

@@ -380,3 +380,96 @@ def test_linear_rows_kp(torch, oracle_model, M):
     q, s2 = O.quant_rows(O.layer_norm(x, la, lb))
     np.testing.assert_array_equal(_from_kp(lnq.cpu().numpy(), M), q)
     np.testing.assert_array_equal(lns.cpu().numpy(), s2)
+
+
+def _ws_pack_ref(w):
+    """The WS order of qtx_pack_w_ws (include/qtx.h), restated in numpy: 1 KB block
+    ((t*8 + w)*8 + s)*4 + j, lane l: W[512t + 64w + 16((l & 15) >> 2) + 4j + (l & 3)]
+    [64s + 16(l >> 4) .. +16]."""
+    N, K = w.shape
+    t, wv, s, j, l = np.meshgrid(np.arange(N // 512), np.arange(8), np.arange(8), np.arange(4),
+                                 np.arange(64), indexing="ij")
+    n = 512 * t + 64 * wv + 16 * ((l & 15) >> 2) + 4 * j + (l & 3)
+    k0 = 64 * s + 16 * (l >> 4)
+    rows = w[n.reshape(-1)]                                  # [chunks, K]
+    idx = k0.reshape(-1)[:, None] + np.arange(16)[None, :]
+    return np.take_along_axis(rows, idx, axis=1).reshape(N, K)
+
+
+def test_pack_w_ws(torch):
+    rng = np.random.default_rng(5)
+    w = rng.integers(-127, 128, (1024, 512)).astype(np.int8)
+    out = torch.empty((1024, 512), dtype=torch.int8, device="cuda")
+    from qtx._lib import lib
+    assert lib().qtx_pack_w_ws(P(dev(torch, w)), 1024, 512, P(out), S0) == 0
+    np.testing.assert_array_equal(out.cpu().numpy(), _ws_pack_ref(w))
+    assert lib().qtx_pack_w_ws(P(dev(torch, w)), 1024, 256, P(out), S0) != 0   # K != 512
+
+
+@pytest.mark.parametrize("M,nopipe", [(300, 0), (7, 0), (64, 0), (20011, 0), (20011, 1)])
+def test_linear_rows_ws(torch, oracle_model, monkeypatch, M, nopipe):
+    """kp = 2 (weight-stationary, K = 512): every epilogue bit-exact against the oracle —
+    Q/K/V per-token quant (row-major out), FFN1 row maxima + hidden quant (KP out), O-proj
+    residual + LayerNorm + quant (KP out) and its fp32 variant; M = 20011 runs several row
+    blocks per workgroup and a ragged last block.  nopipe: the unpipelined 64-row kernel
+    (QTX_WS_NOPIPE; RE_RES_LN always runs on it)."""
+    from qtx._lib import lib
+    if nopipe:
+        monkeypatch.setenv("QTX_WS_NOPIPE", "1")
+    rng = np.random.default_rng(M + 7)
+
+    def weights(N):
+        qw, sw = O.quant_weight((rng.standard_normal((N, 512)) * 0.05).astype(f32), 8)
+        wk = torch.empty((N, 512), dtype=torch.int8, device="cuda")
+        assert lib().qtx_pack_w_ws(P(dev(torch, qw)), N, 512, P(wk), S0) == 0
+        return qw, sw, wk, rng.standard_normal(N).astype(f32)
+
+    qx, sx = O.quant_rows(rng.standard_normal((M, 512)).astype(f32))
+    ax = dev(torch, _to_kp(qx))
+    # epi 0 (QKV)
+    qw, sw, wk, b = weights(1536)
+    out8 = torch.empty((3, M, 512), dtype=torch.int8, device="cuda")
+    os_ = torch.empty((3, M), dtype=torch.float32, device="cuda")
+    _rows_call(torch, A=ax, sa=dev(torch, sx), W=wk, sw=dev(torch, sw), bias=dev(torch, b),
+               M=M, N=1536, K=512, epi=0, out8=out8, ldo8=512, o8_ts=M * 512, os=os_,
+               os_ts=M, kp=2)
+    y = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b)
+    for t in range(3):
+        q, s = O.quant_rows(y[:, 512 * t:512 * (t + 1)])
+        np.testing.assert_array_equal(out8[t].cpu().numpy(), q)
+        np.testing.assert_array_equal(os_[t].cpu().numpy(), s)
+    # epi 2 + 3 (FFN1), hidden written KP
+    qw, sw, wk, b = weights(2048)
+    pm = torch.empty((4, M), dtype=torch.float32, device="cuda")
+    base = dict(A=ax, sa=dev(torch, sx), W=wk, sw=dev(torch, sw), bias=dev(torch, b),
+                M=M, N=2048, K=512, kp=2)
+    _rows_call(torch, epi=2, pmax_out=pm, **base)
+    h = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b, relu=True)
+    np.testing.assert_array_equal(pm.cpu().numpy(), h.reshape(M, 4, 512).max(-1).T)
+    h8 = torch.zeros((M + (M & 1), 2048), dtype=torch.int8, device="cuda")
+    sh = torch.empty(M, dtype=torch.float32, device="cuda")
+    _rows_call(torch, epi=3, pmax_in=pm, pmax_n=4, out8=h8, ldo8=2048, os=sh, **base)
+    qh, s = O.quant_rows(h)
+    np.testing.assert_array_equal(_from_kp(h8.cpu().numpy(), M), qh)
+    np.testing.assert_array_equal(sh.cpu().numpy(), s)
+    # epi 1 (O-proj), next LayerNorm quantized KP, then the fp32 LayerNorm output variant
+    qw, sw, wk, b = weights(512)
+    res = (rng.standard_normal((M, 512)) * 2).astype(f32)
+    la, lb = oracle_model.dec[1]["ln"][0]
+    xd = dev(torch, res.copy())
+    lnq = torch.zeros((M + (M & 1), 512), dtype=torch.int8, device="cuda")
+    lns = torch.empty(M, dtype=torch.float32, device="cuda")
+    obase = dict(A=ax, sa=dev(torch, sx), W=wk, sw=dev(torch, sw), bias=dev(torch, b), M=M,
+                 N=512, K=512, epi=1, ln_a=dev(torch, la), ln_b=dev(torch, lb), kp=2)
+    _rows_call(torch, res=xd, xout=xd, lnq=lnq, lns=lns, **obase)
+    x = res + O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b)
+    np.testing.assert_array_equal(xd.cpu().numpy(), x)
+    ln = O.layer_norm(x, la, lb)
+    q, s2 = O.quant_rows(ln)
+    np.testing.assert_array_equal(_from_kp(lnq.cpu().numpy(), M), q)
+    np.testing.assert_array_equal(lns.cpu().numpy(), s2)
+    xd2 = dev(torch, res.copy())
+    lnout = torch.empty((M, 512), dtype=torch.float32, device="cuda")
+    _rows_call(torch, res=xd2, xout=xd2, lnout=lnout, **obase)
+    np.testing.assert_array_equal(xd2.cpu().numpy(), x)
+    np.testing.assert_array_equal(lnout.cpu().numpy(), ln)
