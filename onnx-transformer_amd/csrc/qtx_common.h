@@ -32,10 +32,21 @@ static __device__ unsigned long long* qtx_stamp_buf;
       qtx_stamp_buf[(blockIdx.y * gridDim.x + blockIdx.x) * 16 + (slot)] =                \
           __builtin_amdgcn_s_memtime();                                                   \
   } while (0)
+// accumulated phase times: QTX_NOW() reads the clock, QTX_STAMP_VAL stores a value
+#define QTX_NOW() ((long long)__builtin_amdgcn_s_memtime())
+#define QTX_STAMP_VAL(slot, v)                                                          \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && qtx_stamp_buf)                                                \
+      qtx_stamp_buf[(blockIdx.y * gridDim.x + blockIdx.x) * 16 + (slot)] = (v);           \
+  } while (0)
 #else
 #define QTX_STAMP_SETTER(unit)
 #define QTX_STAMP(slot) \
   do {                  \
+  } while (0)
+#define QTX_NOW() 0LL
+#define QTX_STAMP_VAL(slot, v) \
+  do {                         \
   } while (0)
 #endif
 

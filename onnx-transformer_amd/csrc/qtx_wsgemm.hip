@@ -607,6 +607,8 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
   };
 
   // ---- block 0: main loop only
+  long long st_top = 0, st_mid = 0, st_h1 = 0, st_h2 = 0;   // QTX_STAMPS builds only
+  const long long st_0 = QTX_NOW();
   v4i accp[2][4];
   float sap, pmp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
@@ -618,8 +620,12 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
   mfma_steps(accp, lds, 0, 8);
   __builtin_amdgcn_s_waitcnt(WAIT_VM(0));   // block 1's DMA (no stores behind it yet)
   // ---- steady state: block k's MFMAs with block k-1's epilogue
+  const long long st_1 = QTX_NOW();
   for (int k = 1; k < nblk; ++k) {
+    const long long t0 = QTX_NOW();
     top_wait();
+    const long long t1 = QTX_NOW();
+    st_top += t1 - t0;
     // last iteration's per-row loads complete HERE, before this iteration's loads and DMA:
     // the compiler's wait for them at their use would otherwise count only its own younger
     // loads and also wait for the DMA issued in between
@@ -635,10 +641,15 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
     float y[2][16];
     mfma_steps(acc, cur, 0, 4);
     epi1(accp, sap, y);
+    const long long t2 = QTX_NOW();
+    st_h1 += t2 - t1;
     __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
     __builtin_amdgcn_s_barrier();
+    const long long t3 = QTX_NOW();
+    st_mid += t3 - t2;
     mfma_steps(acc, cur, 4, 8);
     epi2(k - 1, y, pmp);
+    st_h2 += QTX_NOW() - t3;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -657,6 +668,14 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
     epi2(nblk - 1, y, pmp);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // phase totals for tools/wsp_stamps.py (QTX_STAMPS builds only)
+  QTX_STAMP_VAL(0, st_1 - st_0);
+  QTX_STAMP_VAL(1, st_top);
+  QTX_STAMP_VAL(2, st_h1);
+  QTX_STAMP_VAL(3, st_mid);
+  QTX_STAMP_VAL(4, st_h2);
+  QTX_STAMP_VAL(5, QTX_NOW() - st_0);
+  QTX_STAMP_VAL(6, nblk);
 }
 
 hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {
