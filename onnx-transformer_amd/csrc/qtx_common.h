@@ -177,10 +177,19 @@ __device__ __forceinline__ bool divisor_ok(float b) {
   return m - 0x30800001u < 0x4e800000u - 0x30800001u;   // 2^-30 < |b| < 2^30
 }
 
+// RN(a / b) for a divisor known at compile time (y = RN(1/b) is folded): div_cr when a is
+// in its range (any lane outside -> the true division, a wave-uniform vote), i.e. the IEEE
+// quotient without the ~10-instruction division sequence on the dependent chain.
+__device__ __forceinline__ float div_const(float a, float b) {
+  const float y = 1.0f / b;
+  if (__builtin_expect(__ballot(!div_ok(a)) == 0ull, 1)) return div_cr(a, b, y);
+  return a / b;
+}
+
 // ---------------------------------------------------------------- quantizer
 // quant_linear.py:30-43 / :5-17:  s = max(absmax, 1e-5) / qmax;  q = rint(x / s).
 __device__ __forceinline__ float quant_scale(float absmax, float qmax) {
-  return fmaxf(absmax, 1e-5f) / qmax;
+  return div_const(fmaxf(absmax, 1e-5f), qmax);
 }
 __device__ __forceinline__ int quant_val(float x, float s) { return (int)rintf(x / s); }
 
@@ -215,10 +224,12 @@ __device__ __forceinline__ uint32_t pack4_biased(float t0, float t1, float t2, f
 // tie both round to the same integer.
 // The near-tie test is folded over all of a lane's values and voted across the wave, so
 // the division runs behind ONE wave-uniform branch that is almost never taken.
+// The reciprocal is v_rcp_f32 (within 1 ulp): r is then within 2^-15.5 of x/s, inside the
+// 2^-13 tie window, so the rounding decision is unchanged.
 template <int N>
 __device__ __forceinline__ void quant_pack(const float* x, float s, uint32_t* out) {
   static_assert(N % 4 == 0, "groups of 4");
-  const float inv = 1.0f / s;
+  const float inv = __builtin_amdgcn_rcpf(s);
   float r[N];
   bool near = false;
 #pragma unroll
@@ -237,7 +248,7 @@ __device__ __forceinline__ void quant_pack(const float* x, float s, uint32_t* ou
 }
 // single value per lane
 __device__ __forceinline__ int quant_one(float x, float s) {
-  float r = x * (1.0f / s);
+  float r = x * __builtin_amdgcn_rcpf(s);
   const bool near = fabsf((r - floorf(r)) - 0.5f) < 0x1p-13f;
   if (__builtin_expect(__ballot(near) != 0ull, 0)) r = x / s;
   return (int)rintf(r);
@@ -280,7 +291,7 @@ __device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float (&ga
     den[j] = ss;
   }
 #pragma unroll
-  for (int j = 0; j < R; ++j) den[j] = sqrtf(wave_sum(den[j]) / 511.0f) + 1e-6f;
+  for (int j = 0; j < R; ++j) den[j] = sqrtf(div_const(wave_sum(den[j]), 511.0f)) + 1e-6f;
   // y = (a * d) / den + b, the division correctly rounded via div_cr (one true division
   // per row for the reciprocal), true division if any value is outside div_cr's range
   DivRange rg;
