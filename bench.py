@@ -118,12 +118,28 @@ def pmc_traffic():
         return json.load(f).get("traffic_bytes_per_launch")
 
 
-def time_row_gemms(M=256 * 128, reps=10, ws=True):
+def _quantized_rows(rng, M, K, relu=False):
+    """int8 rows distributed as the encoder's activations: per-token absmax quantization
+    (quant_linear.py:30-43) of Gaussian rows (LayerNorm outputs), or of ReLU'd Gaussian
+    rows (the FFN hidden) — most codes small, the row maximum at 127."""
+    g = rng.standard_normal((M, K), dtype=np.float32)
+    if relu:
+        g = np.maximum(g, 0.0)
+    s = np.maximum(np.abs(g).max(1, keepdims=True), 1e-5) / 127.0
+    return np.rint(g / s).astype(np.int8)
+
+
+def time_row_gemms(M=256 * 128, reps=10, ws=True, operands="encoder"):
     """The five QuantLinear launches of one cfg3 encoder layer through qtx_linear_rows on
     synthetic int8 operands (QKV + per-token quant, O + residual + LN + quant, FFN1 row-max
     pass, FFN1 ReLU + quant pass, FFN2 + residual + LN + quant): (us per launch, ops).
     ws: the Q/K/V and FFN1 launches on the weight-stationary kernel (kp = 2), as the encoder
-    runs them at this M (csrc/qtx_api.hip rowgemm); O and FFN2 on the KP row GEMM."""
+    runs them at this M (csrc/qtx_api.hip rowgemm); O and FFN2 on the KP row GEMM.
+    operands: "encoder" = activations per-token quantized from Gaussian (ReLU'd for FFN2)
+    rows and weights uniform over [-127, 127] (what per-channel quantization of the
+    Xavier-uniform synthetic weights gives) — the encoder's own operand statistics;
+    "uniform" = every operand uniform over [-127, 127], the MFMA power worst case (the
+    matrix-core clock drops with operand toggling)."""
     import ctypes as C
 
     import torch
@@ -132,8 +148,12 @@ def time_row_gemms(M=256 * 128, reps=10, ws=True):
     L = _lib.lib(build=False)
     rng = np.random.default_rng(0)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
-    a512 = T(rng.integers(-127, 128, (M, D)).astype(np.int8))
-    a2048 = T(rng.integers(-127, 128, (M, F)).astype(np.int8))
+    if operands == "uniform":
+        a512 = T(rng.integers(-127, 128, (M, D)).astype(np.int8))
+        a2048 = T(rng.integers(-127, 128, (M, F)).astype(np.int8))
+    else:
+        a512 = T(_quantized_rows(rng, M, D))
+        a2048 = T(_quantized_rows(rng, M, F, relu=True))
     sa = torch.full((M,), 0.01, device="cuda")
     W = {nk: T(rng.integers(-127, 128, nk).astype(np.int8)) for nk in [(3 * D, D), (D, D), (F, D), (D, F)]}
     sw = torch.full((F,), 0.01, device="cuda")
@@ -381,8 +401,11 @@ def main():
                 "B": Bc, "S": Sc, "ms": te * 1e3, "quantlinear_int8_ops": ops,
                 "whole_encoder_ops_per_s": ops / te,
                 "frac_of_int8_peak_whole_encoder": ops / te / PEAK_INT8_OPS,
-                # the layer's QuantLinear launches alone, KP instances (algorithmic ops:
-                # FFN1 counted once although its per-token quantization needs two passes)
+                # the layer's QuantLinear launches alone, as the encoder runs them (WS / KP
+                # instances; algorithmic ops: FFN1 counted once although its per-token
+                # quantization needs two passes), on operands with the encoder's statistics
+                # (per-token quantized activations; uniform random bytes measured the same
+                # within 2 %, profiles/r02j_pmc_encoder.json's note)
                 "gemm_us_per_layer": {k: round(t, 1) for k, (t, _) in g.items()},
                 "frac_of_int8_peak_quantlinear_gemms": gemm_ops / (gemm_us * 1e-6) / PEAK_INT8_OPS}
             # BASELINE configs 4 and 5 (secondary lines): int4 weights at B=32, and the
