@@ -37,55 +37,16 @@ __device__ __forceinline__ uint4 unpack_i4(uint2 h) {
 // =====================================================================================
 // k_skinny
 // =====================================================================================
-template <int MF, int RB, int K, int WBITS, int AMODE, int FLAGS>
-__global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
-  constexpr int BM = 16 * MF;     // MFMA rows (rows >= RB of the A panel are don't-care)
-  static_assert(RB % 4 == 0 && RB <= BM, "rows per block");
-  constexpr int KW = K / 4;       // K range of one wave
-  constexpr int NS = KW / 64;     // MFMA k-steps per wave
-  constexpr int LDA = K + 16;     // padded LDS row (bytes)
-  __shared__ __attribute__((aligned(16))) uint8_t As[BM * LDA];
-  __shared__ float sas[BM];
-  __shared__ v4i red[3][MF][64];
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * RB;
-
-  QTX_STAMP(0);
-
-  // 1. this lane's W fragments for its wave's K range, issued first
-  const int n = min(n0 + fr, g.N - 1);
-  uint4 wf[NS];
-  uint2 wp[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int k = wave * KW + 64 * s + 16 * fg;
-    if constexpr (WBITS == 8)
-      wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + k);
-    else
-      wp[s] = *reinterpret_cast<const uint2*>(g.W + (long)n * g.ldw + (k >> 1));
-  }
-  // epilogue operands of wave 0 (it finishes the tile), also issued up front: a load
-  // first issued after the reduction barrier would add a whole memory round trip
-  const int col = n0 + fr;
-  const bool cok = col < g.N;
-  float swc = 0.0f, bc = 0.0f, rv[MF][4];
-  constexpr bool resid = FLAGS & EPI_RESIDUAL;
-  if (wave == 0) {
-    swc = cok ? g.sw[col] : 0.0f;
-    bc = cok ? g.bias[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < MF; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = 16 * i + 4 * fg + e, row = m0 + r;
-        rv[i][e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
-      }
-  }
-
-  // 2. A panel (int8) and per-row scales into LDS.  Every branch issues all of its
-  //    global loads before consuming any (one memory latency, not one per row).
+// The A operand of a skinny GEMM workgroup (rows m0 .. m0 + RB - 1) into LDS: int8 rows
+// (A_I8), LayerNorm + per-token quant of fp32 rows (A_LN), or per-token quant of fp32 rows
+// from their partial maxima (A_F32Q).  Rows >= M are zero; sas = per-row scales.  Every
+// branch issues all of its global loads before consuming any (one memory latency, not one
+// per row).  Wave w takes rows w, w + 4, ...
+template <int RB, int K, int AMODE>
+__device__ __forceinline__ void skinny_prologue(const SkinnyArgs& g, uint8_t* As, float* sas,
+                                                int m0, int tid, int wave, int lane) {
+  constexpr int LDA = K + 16;
+  constexpr int BM = RB <= 16 ? 16 : 32;
   constexpr int RPW = RB / 4;  // rows per wave: r = wave + 4*j
   if constexpr (AMODE == A_I8) {
     // the panel is RB*K/16 uint4; the index is clamped (a duplicate load, no divergent
@@ -165,6 +126,57 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
       }
     }
   }
+}
+
+template <int MF, int RB, int K, int WBITS, int AMODE, int FLAGS>
+__global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
+  constexpr int BM = 16 * MF;     // MFMA rows (rows >= RB of the A panel are don't-care)
+  static_assert(RB % 4 == 0 && RB <= BM, "rows per block");
+  constexpr int KW = K / 4;       // K range of one wave
+  constexpr int NS = KW / 64;     // MFMA k-steps per wave
+  constexpr int LDA = K + 16;     // padded LDS row (bytes)
+  __shared__ __attribute__((aligned(16))) uint8_t As[BM * LDA];
+  __shared__ float sas[BM];
+  __shared__ v4i red[3][MF][64];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * RB;
+
+  QTX_STAMP(0);
+
+  // 1. this lane's W fragments for its wave's K range, issued first
+  const int n = min(n0 + fr, g.N - 1);
+  uint4 wf[NS];
+  uint2 wp[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int k = wave * KW + 64 * s + 16 * fg;
+    if constexpr (WBITS == 8)
+      wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + k);
+    else
+      wp[s] = *reinterpret_cast<const uint2*>(g.W + (long)n * g.ldw + (k >> 1));
+  }
+  // epilogue operands of wave 0 (it finishes the tile), also issued up front: a load
+  // first issued after the reduction barrier would add a whole memory round trip
+  const int col = n0 + fr;
+  const bool cok = col < g.N;
+  float swc = 0.0f, bc = 0.0f, rv[MF][4];
+  constexpr bool resid = FLAGS & EPI_RESIDUAL;
+  if (wave == 0) {
+    swc = cok ? g.sw[col] : 0.0f;
+    bc = cok ? g.bias[col] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 16 * i + 4 * fg + e, row = m0 + r;
+        rv[i][e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
+      }
+  }
+
+  // 2. A panel (int8) and per-row scales into LDS
+  skinny_prologue<RB, K, AMODE>(g, As, sas, m0, tid, wave, lane);
   __syncthreads();
 
   QTX_STAMP(1);
@@ -225,6 +237,109 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
   QTX_STAMP(3);
 }
 
+// =====================================================================================
+// k_skinny_wide: the K = 512 skinny GEMM with N split over the 4 waves instead of K — a
+// workgroup covers 64 columns (wave w: columns n0 + 16w .. +15, all 8 K steps, 8 weight
+// fragments = 128 B per lane in flight) and its RB rows; no cross-wave reduction.  The
+// prologue (LayerNorm + quant of the RB rows, or their per-token quant) then serves 64
+// columns instead of 16: 4x fewer redundant LayerNorms per launch.  Same int32 sums, same
+// epilogue arithmetic: bit-identical to k_skinny.
+// =====================================================================================
+template <int RB, int WBITS, int AMODE, int FLAGS>
+__global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
+  constexpr int K = 512, NS = K / 64, LDA = K + 16;
+  static_assert(RB % 4 == 0 && RB <= 16, "rows per block");
+  __shared__ __attribute__((aligned(16))) uint8_t As[16 * LDA];
+  __shared__ float sas[16];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int n0 = blockIdx.x * 64 + 16 * wave, m0 = blockIdx.y * RB;
+  QTX_STAMP(0);
+  // 1. this lane's W fragments (all of K), issued first
+  const int n = min(n0 + fr, g.N - 1);
+  uint4 wf[NS];
+  uint2 wp[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int k = 64 * s + 16 * fg;
+    if constexpr (WBITS == 8)
+      wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + k);
+    else
+      wp[s] = *reinterpret_cast<const uint2*>(g.W + (long)n * g.ldw + (k >> 1));
+  }
+  // epilogue operands of the wave's 16 columns, also up front
+  const int col = n0 + fr;
+  const bool cok = col < g.N;
+  constexpr bool resid = FLAGS & EPI_RESIDUAL;
+  const float swc = cok ? g.sw[col] : 0.0f;
+  const float bc = cok ? g.bias[col] : 0.0f;
+  float rv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int r = 4 * fg + e, row = m0 + r;
+    rv[e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
+  }
+  // 2. A panel and per-row scales into LDS
+  skinny_prologue<RB, K, AMODE>(g, As, sas, m0, tid, wave, lane);
+  __syncthreads();
+  QTX_STAMP(1);
+  // 3. MFMA over all of K
+  v4i acc = v4i{0, 0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    v4i bfr;
+    if constexpr (WBITS == 8) bfr = __builtin_bit_cast(v4i, wf[s]);
+    else bfr = __builtin_bit_cast(v4i, unpack_i4(wp[s]));
+    const v4i afr = *reinterpret_cast<const v4i*>(As + fr * LDA + 64 * s + 16 * fg);
+    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, bfr, acc, 0, 0, 0);
+  }
+  QTX_STAMP(2);
+  // 4. epilogue (C layout: col = lane & 15, row = 4*(lane>>4) + e)
+  constexpr bool relu = FLAGS & EPI_RELU, rmax = FLAGS & EPI_ROWMAX;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int r = 4 * fg + e, row = m0 + r;
+    const bool ok = cok && r < RB && row < g.M;
+    float y = ((float)acc[e] * sas[r]) * swc + bc;
+    if constexpr (relu) y = y > 0.0f ? y : 0.0f;
+    if constexpr (resid) y = rv[e] + y;
+    if (ok) g.out[(long)row * g.ldo + col] = y;
+    if constexpr (rmax) {
+      float am = ok ? fabsf(y) : 0.0f;   // max over the 16 lanes (columns) of this row
+      am = fmaxf(am, dpp<0xB1>(am));
+      am = fmaxf(am, dpp<0x4E>(am));
+      am = fmaxf(am, dpp<0x141>(am));
+      am = fmaxf(am, dpp<0x140>(am));
+      if (fr == 0 && r < RB && row < g.M) g.pmax_out[(long)(n0 >> 4) * g.M + row] = am;
+    }
+  }
+  QTX_STAMP(3);
+}
+
+template <int RB, int WB, int AM>
+hipError_t skinny_wide_flags(const SkinnyArgs& g, hipStream_t st) {
+  const dim3 grid(g.N / 64, (g.M + RB - 1) / RB);
+  switch (g.flags) {
+    case 0: k_skinny_wide<RB, WB, AM, 0><<<grid, 256, 0, st>>>(g); break;
+    case EPI_RELU: k_skinny_wide<RB, WB, AM, EPI_RELU><<<grid, 256, 0, st>>>(g); break;
+    case EPI_RESIDUAL: k_skinny_wide<RB, WB, AM, EPI_RESIDUAL><<<grid, 256, 0, st>>>(g); break;
+    case EPI_RELU | EPI_ROWMAX:
+      k_skinny_wide<RB, WB, AM, EPI_RELU | EPI_ROWMAX><<<grid, 256, 0, st>>>(g);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+template <int WB, int AM>
+hipError_t skinny_wide_rb(const SkinnyArgs& g, int rb, hipStream_t st) {
+  switch (rb) {
+    case 4: return skinny_wide_flags<4, WB, AM>(g, st);
+    case 8: return skinny_wide_flags<8, WB, AM>(g, st);
+    case 16: return skinny_wide_flags<16, WB, AM>(g, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // dispatch: the prologue mode and epilogue flags are template parameters (no runtime
 // branches per output element).  Supported: K 512 with A_I8 / A_LN, K 2048 with A_I8 /
 // A_F32Q; flags 0, RELU, RESIDUAL, RELU|ROWMAX.  Rows per workgroup RB: 16*MF for an int8
@@ -266,6 +381,19 @@ int env_rb(const char* name, int def) {   // experiment overrides (QTX_RB_*)
 // so a latency-bound kernel is fastest when every workgroup touches ~10-40 KB.
 template <int WB>
 hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
+  // The N-split workgroup (k_skinny_wide) for the LayerNorm-prologue GEMMs with N >= 1024
+  // (LN+QKV, LN+FFN1): measured in the decode graph at M = 32 (tools/kernel_chain.py)
+  // 4.50 -> 3.67 and 5.26 -> 3.95 us per launch; at N = 512 the K-split one is faster
+  // (64 workgroups of 32 KB each vs 256 of 8 KB: 3.09 vs 3.60 us).  QTX_SKINNY_WIDE=0: never,
+  // =<rb>: every K = 512 launch (experiments).
+  static const int wide_env = env_rb("QTX_SKINNY_WIDE", -1);
+  const bool wide = wide_env < 0 ? (g.amode == A_LN && g.N >= 1024) : wide_env > 0;
+  if (wide && g.K == 512 && g.N % 64 == 0) {
+    const int rb = g.M <= 4 || wide_env <= 0 ? 4 : wide_env;
+    if (g.amode == A_I8) return skinny_wide_rb<WB, A_I8>(g, rb, st);
+    if (g.amode == A_LN) return skinny_wide_rb<WB, A_LN>(g, rb, st);
+    if (g.amode == A_F32Q) return skinny_wide_rb<WB, A_F32Q>(g, rb, st);
+  }
   if (g.K == 512) {
     static const int rb_i8 = env_rb("QTX_RB_I8_512", 4), rb_ln = env_rb("QTX_RB_LN", 4);
     if (g.amode == A_I8) return skinny_rb<512, WB, A_I8>(g, g.M <= 4 ? 4 : rb_i8, st);
