@@ -53,42 +53,45 @@ def encoder_gemm_ops(B, S, n_layers=6):
     return n_layers * 2 * M * (3 * D * D + D * D + D * F + F * D)
 
 
-DOMINANT = "k_skinny<1,4,512,8,A_LN,0>"   # LN+QKV GEMM of the decode step (profiles/)
+DOMINANT = "k_skinny<1,4,2048,8,A_F32Q,RESIDUAL>"   # FFN2 GEMM of the decode step (profiles/)
 
 
 def dominant_alg_bytes(B):
-    """Algorithmic bytes of one LN+QKV decode launch: int8 W [1536,512] + fp32 x [B,512] +
-    LN gamma/beta + per-channel scale/bias + fp32 out [B,1536]."""
-    N, K = 3 * D, D
-    return N * K + B * K * 4 + 2 * K * 4 + 2 * N * 4 + B * N * 4
+    """Algorithmic bytes of one FFN2 decode launch (position_feed_forward.py:12 + the
+    residual, sublayer_connection.py:17): int8 W [512, 2048] + fp32 hidden [B, 2048] (quantized
+    per token in the prologue) + its partial row maxima [128, B] + per-channel scale/bias +
+    fp32 residual in and out [B, 512]."""
+    N, K = D, F
+    return N * K + B * K * 4 + (F // 16) * B * 4 + 2 * N * 4 + 2 * B * N * 4
 
 
 def run_dominant(B, iters, stream=None):
     """Launch the decode step's dominant kernel `iters` times (shapes of the real model:
-    M=B rows, N=1536, K=512, LayerNorm prologue).  Returns (launch fn, keepalive)."""
+    M=B rows, N=512, K=2048, per-token quantization of the fp32 hidden from its partial
+    maxima in the prologue, residual epilogue).  Returns (launch fn, keepalive)."""
     import ctypes as C
 
     import torch
 
     from qtx import _lib
     rng = np.random.default_rng(1)
-    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).cuda()
-    lna = torch.ones(D, device="cuda")
-    lnb = torch.zeros(D, device="cuda")
-    w = torch.from_numpy(rng.integers(-127, 128, (3 * D, D)).astype(np.int8)).cuda()
-    sw = torch.full((3 * D,), 0.01, device="cuda")
-    bias = torch.zeros(3 * D, device="cuda")
-    out = torch.empty((B, 3 * D), device="cuda")
+    h = torch.from_numpy(np.maximum(rng.standard_normal((B, F)), 0).astype(np.float32)).cuda()
+    pm = h.abs().reshape(B, F // 16, 16).amax(-1).t().contiguous()   # [F/16][B]
+    w = torch.from_numpy(rng.integers(-127, 128, (D, F)).astype(np.int8)).cuda()
+    sw = torch.full((D,), 0.01, device="cuda")
+    bias = torch.zeros(D, device="cuda")
+    res = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).cuda()
+    out = torch.empty((B, D), device="cuda")
     st = C.c_void_p(stream if stream is not None else torch.cuda.current_stream().cuda_stream)
     P = lambda t: C.c_void_p(t.data_ptr())
     S0 = C.c_void_p(0)
-    args = (1, S0, S0, P(x), D, P(lna), P(lnb), S0, 0, P(w), P(sw), P(bias), B, 3 * D, D, 8, 0,
-            S0, P(out), S0, st)
+    args = (2, S0, S0, P(h), F, S0, S0, P(pm), F // 16, P(w), P(sw), P(bias), B, D, F, 8, 2,
+            P(res), P(out), S0, st)
 
     def launch():
         for _ in range(iters):
             _lib.call("qtx_skinny_linear", *args)
-    return launch, (x, lna, lnb, w, sw, bias, out)
+    return launch, (h, pm, w, sw, bias, res, out)
 
 
 def time_dominant(B, iters=200):
@@ -352,7 +355,7 @@ def main():
     if rank == 0:
         kt = time_dominant(min(B, 32))
         alg = dominant_alg_bytes(min(B, 32))
-        roof = {"kernel": f"{DOMINANT}: LN+QKV decode GEMM (M={min(B, 32)}, N={3 * D}, K={D}, int8)",
+        roof = {"kernel": f"{DOMINANT}: FFN2 decode GEMM (M={min(B, 32)}, N={D}, K={F}, int8)",
                 "bound": "hbm", "achieved": alg / kt / 1e9, "peak": PEAK_HBM / 1e9,
                 "unit": "GB/s", "frac": alg / kt / PEAK_HBM, "traffic": pmc_traffic(),
                 "avg_us": kt * 1e6, "alg_bytes_per_launch": alg}
