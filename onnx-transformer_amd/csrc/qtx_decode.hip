@@ -41,10 +41,15 @@ __device__ __forceinline__ uint4 unpack_i4(uint2 h) {
 // (A_I8), LayerNorm + per-token quant of fp32 rows (A_LN), or per-token quant of fp32 rows
 // from their partial maxima (A_F32Q).  Rows >= M are zero; sas = per-row scales.  Every
 // branch issues all of its global loads before consuming any (one memory latency, not one
-// per row).  Wave w takes rows w, w + 4, ...
-template <int RB, int K, int AMODE>
+// per row).  Wave w takes rows w, w + 4, ...  issue_rest() (the weight fragments and the
+// epilogue operands) is called right after the A operand's loads are issued: vmcnt retires
+// in issue order, so the LayerNorm / quantization then waits for its own rows only and
+// runs while the weights are in flight (measured: issuing the weights first made the two
+// latencies add up, ~0.7 us per launch).
+template <int RB, int K, int AMODE, class F>
 __device__ __forceinline__ void skinny_prologue(const SkinnyArgs& g, uint8_t* As, float* sas,
-                                                int m0, int tid, int wave, int lane) {
+                                                int m0, int tid, int wave, int lane,
+                                                F&& issue_rest) {
   constexpr int LDA = K + 16;
   constexpr int BM = RB <= 16 ? 16 : 32;
   constexpr int RPW = RB / 4;  // rows per wave: r = wave + 4*j
@@ -58,6 +63,7 @@ __device__ __forceinline__ void skinny_prologue(const SkinnyArgs& g, uint8_t* As
       const int idx = min(tid + 256 * j, TOT - 1), m = min(m0 + idx / CPR, g.M - 1);
       v[j] = *reinterpret_cast<const uint4*>(g.A + (long)m * K + 16 * (idx % CPR));
     }
+    issue_rest();
     if (tid < BM) sas[tid] = (tid < RB && m0 + tid < g.M) ? g.sa[m0 + tid] : 0.0f;
 #pragma unroll
     for (int j = 0; j < NLD; ++j) {
@@ -77,10 +83,20 @@ __device__ __forceinline__ void skinny_prologue(const SkinnyArgs& g, uint8_t* As
         v[j][c][0] = t.x; v[j][c][1] = t.y; v[j][c][2] = t.z; v[j][c][3] = t.w;
       }
     }
-    ln_rows512<RPW>(v, g.ln_a, g.ln_b, lane);
+    float ga[2][4], gb[2][4];
+    ln_params512(g.ln_a, g.ln_b, lane, ga, gb);
+    issue_rest();
     uint32_t q[RPW][2];
     float sc[RPW];
+#if defined(QTX_ABL) && (QTX_ABL & 2)   // diagnostic builds only: no LayerNorm / quant chain
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      q[j][0] = __float_as_uint(v[j][0][0]); q[j][1] = __float_as_uint(v[j][1][0]); sc[j] = v[j][0][1];
+    }
+#else
+    ln_rows512<RPW>(v, ga, gb);
     quant_rows512<RPW>(v, q, sc);
+#endif
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       const int r = wave + 4 * j;
@@ -106,6 +122,7 @@ __device__ __forceinline__ void skinny_prologue(const SkinnyArgs& g, uint8_t* As
         for (int u = 0; u < 2; ++u)   // lane takes partials lane, lane+64 (clamped: max-safe)
           pm[jb][u] = g.pmax_in[(long)min(lane + 64 * u, g.pmax_n - 1) * g.M + m];
       }
+      if (j0 == 0) issue_rest();
 #pragma unroll
       for (int jb = 0; jb < RBT; ++jb) {
         const int r = wave + 4 * (j0 + jb);
@@ -145,38 +162,40 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
 
   QTX_STAMP(0);
 
-  // 1. this lane's W fragments for its wave's K range, issued first
+  // 1. this lane's W fragments for its wave's K range, and the epilogue operands of wave 0
+  //    (it finishes the tile: a load first issued after the reduction barrier would add a
+  //    whole memory round trip) — issued right after the A operand's loads (prologue)
   const int n = min(n0 + fr, g.N - 1);
   uint4 wf[NS];
   uint2 wp[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int k = wave * KW + 64 * s + 16 * fg;
-    if constexpr (WBITS == 8)
-      wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + k);
-    else
-      wp[s] = *reinterpret_cast<const uint2*>(g.W + (long)n * g.ldw + (k >> 1));
-  }
-  // epilogue operands of wave 0 (it finishes the tile), also issued up front: a load
-  // first issued after the reduction barrier would add a whole memory round trip
   const int col = n0 + fr;
   const bool cok = col < g.N;
   float swc = 0.0f, bc = 0.0f, rv[MF][4];
   constexpr bool resid = FLAGS & EPI_RESIDUAL;
-  if (wave == 0) {
-    swc = cok ? g.sw[col] : 0.0f;
-    bc = cok ? g.bias[col] : 0.0f;
+  auto issue_rest = [&]() {
 #pragma unroll
-    for (int i = 0; i < MF; ++i)
+    for (int s = 0; s < NS; ++s) {
+      const int k = wave * KW + 64 * s + 16 * fg;
+      if constexpr (WBITS == 8)
+        wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + k);
+      else
+        wp[s] = *reinterpret_cast<const uint2*>(g.W + (long)n * g.ldw + (k >> 1));
+    }
+    if (wave == 0) {
+      swc = cok ? g.sw[col] : 0.0f;
+      bc = cok ? g.bias[col] : 0.0f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = 16 * i + 4 * fg + e, row = m0 + r;
-        rv[i][e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
-      }
-  }
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 16 * i + 4 * fg + e, row = m0 + r;
+          rv[i][e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
+        }
+    }
+  };
 
   // 2. A panel (int8) and per-row scales into LDS
-  skinny_prologue<RB, K, AMODE>(g, As, sas, m0, tid, wave, lane);
+  skinny_prologue<RB, K, AMODE>(g, As, sas, m0, tid, wave, lane, issue_rest);
   __syncthreads();
 
   QTX_STAMP(1);
@@ -255,32 +274,38 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
   const int fr = lane & 15, fg = lane >> 4;
   const int n0 = blockIdx.x * 64 + 16 * wave, m0 = blockIdx.y * RB;
   QTX_STAMP(0);
-  // 1. this lane's W fragments (all of K), issued first
+  // 1. this lane's W fragments (all of K) and the epilogue operands of the wave's 16
+  //    columns — issued right after the A operand's loads (prologue)
   const int n = min(n0 + fr, g.N - 1);
   uint4 wf[NS];
   uint2 wp[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int k = 64 * s + 16 * fg;
-    if constexpr (WBITS == 8)
-      wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + k);
-    else
-      wp[s] = *reinterpret_cast<const uint2*>(g.W + (long)n * g.ldw + (k >> 1));
-  }
-  // epilogue operands of the wave's 16 columns, also up front
   const int col = n0 + fr;
   const bool cok = col < g.N;
   constexpr bool resid = FLAGS & EPI_RESIDUAL;
-  const float swc = cok ? g.sw[col] : 0.0f;
-  const float bc = cok ? g.bias[col] : 0.0f;
-  float rv[4];
+  float swc, bc, rv[4];
+  auto issue_rest = [&]() {
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int r = 4 * fg + e, row = m0 + r;
-    rv[e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
-  }
+    for (int s = 0; s < NS; ++s) {
+      const int k = 64 * s + 16 * fg;
+#if defined(QTX_ABL) && (QTX_ABL & 1)   // diagnostic builds only: no weight loads
+      wf[s] = make_uint4(n + k, k, n, 1); wp[s] = make_uint2(n, k);
+#else
+      if constexpr (WBITS == 8)
+        wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + k);
+      else
+        wp[s] = *reinterpret_cast<const uint2*>(g.W + (long)n * g.ldw + (k >> 1));
+#endif
+    }
+    swc = cok ? g.sw[col] : 0.0f;
+    bc = cok ? g.bias[col] : 0.0f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = 4 * fg + e, row = m0 + r;
+      rv[e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
+    }
+  };
   // 2. A panel and per-row scales into LDS
-  skinny_prologue<RB, K, AMODE>(g, As, sas, m0, tid, wave, lane);
+  skinny_prologue<RB, K, AMODE>(g, As, sas, m0, tid, wave, lane, issue_rest);
   __syncthreads();
   QTX_STAMP(1);
   // 3. MFMA over all of K
@@ -291,7 +316,11 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
     if constexpr (WBITS == 8) bfr = __builtin_bit_cast(v4i, wf[s]);
     else bfr = __builtin_bit_cast(v4i, unpack_i4(wp[s]));
     const v4i afr = *reinterpret_cast<const v4i*>(As + fr * LDA + 64 * s + 16 * fg);
+#if defined(QTX_ABL) && (QTX_ABL & 4)   // diagnostic builds only: no matrix work
+    acc += afr ^ bfr;
+#else
     acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, bfr, acc, 0, 0, 0);
+#endif
   }
   QTX_STAMP(2);
   // 4. epilogue (C layout: col = lane & 15, row = 4*(lane>>4) + e)
