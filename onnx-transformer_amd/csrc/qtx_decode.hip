@@ -468,8 +468,23 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   const int nrows = KV_NEW ? (int)a.kv_bs : a.S;   // rows staged (self: all allocated rows)
   const long kvb = (long)b * a.kv_bs;
 
-  // phase 0: every global load first (one memory latency).  Key/value row r of this head
-  // = 4 uint4; lane takes row 16*i + lane/4, chunk lane%4 (clamped: no divergent loads).
+  // phase 0: every global load first (one memory latency): this step's q (k, v) rows
+  // first — vmcnt retires in issue order, so their quantization (phase 1) then runs while
+  // the cached keys and values are in flight — then the key/value rows of this head (row r
+  // = 4 uint4; lane takes row 16*i + lane/4, chunk lane%4; clamped: no divergent loads)
+  float4 yq[2], yk[2], yv[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    yq[c] = *reinterpret_cast<const float4*>(yr + 4 * (lane + 64 * c));
+    if constexpr (KV_NEW) {
+      yk[c] = *reinterpret_cast<const float4*>(yr + 512 + 4 * (lane + 64 * c));
+      yv[c] = *reinterpret_cast<const float4*>(yr + 1024 + 4 * (lane + 64 * c));
+    }
+  }
+  const float q_own = yr[h * 64 + lane];
+  const float k_own = KV_NEW ? yr[512 + h * 64 + lane] : 0.0f;
+  const float v_own = KV_NEW ? yr[1024 + h * 64 + lane] : 0.0f;
+  const int step = KV_NEW ? *a.step : 0;
   const int rsub = lane >> 2, ch = lane & 3;
   uint4 kr[NIT], vr[NIT];
 #pragma unroll
@@ -487,19 +502,6 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
     keep0 = a.mask[(long)b * a.S + j0] != 0;
     keep1 = a.mask[(long)b * a.S + j1] != 0;
   }
-  float4 yq[2], yk[2], yv[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    yq[c] = *reinterpret_cast<const float4*>(yr + 4 * (lane + 64 * c));
-    if constexpr (KV_NEW) {
-      yk[c] = *reinterpret_cast<const float4*>(yr + 512 + 4 * (lane + 64 * c));
-      yv[c] = *reinterpret_cast<const float4*>(yr + 1024 + 4 * (lane + 64 * c));
-    }
-  }
-  const float q_own = yr[h * 64 + lane];
-  const float k_own = KV_NEW ? yr[512 + h * 64 + lane] : 0.0f;
-  const float v_own = KV_NEW ? yr[1024 + h * 64 + lane] : 0.0f;
-  const int step = KV_NEW ? *a.step : 0;
   // cross: keys past the sentence's last unmasked one contribute exactly nothing (score
   // -1e9 -> qexp 0 -> P 0, and fma(0, v, acc) == acc), so the key loops stop there; a
   // fully masked row keeps all S keys (the reference's uniform softmax over -1e9 scores)
