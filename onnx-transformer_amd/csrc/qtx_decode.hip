@@ -136,7 +136,12 @@ __device__ __forceinline__ void skinny_prologue(const SkinnyArgs& g, uint8_t* As
           tf[4 * c + 2] = t[jb][c].z; tf[4 * c + 3] = t[jb][c].w;
         }
         uint32_t qd[NC];
+#if defined(QTX_ABL) && (QTX_ABL & 8)   // diagnostic builds only: no per-token quantization
+#pragma unroll
+        for (int c = 0; c < NC; ++c) qd[c] = __float_as_uint(tf[4 * c] * sc);
+#else
         quant_pack<4 * NC>(tf, sc, qd);
+#endif
 #pragma unroll
         for (int c = 0; c < NC; ++c) dst[lane + 64 * c] = ok ? qd[c] : 0u;
         if (lane == 0) sas[r] = ok ? sc : 0.0f;
@@ -176,20 +181,28 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int k = wave * KW + 64 * s + 16 * fg;
+#if defined(QTX_ABL) && (QTX_ABL & 1)   // diagnostic builds only: no weight loads
+      wf[s] = make_uint4(n + k, k, n, 1); wp[s] = make_uint2(n, k);
+#else
       if constexpr (WBITS == 8)
         wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + k);
       else
         wp[s] = *reinterpret_cast<const uint2*>(g.W + (long)n * g.ldw + (k >> 1));
+#endif
     }
-    if (wave == 0) {
-      swc = cok ? g.sw[col] : 0.0f;
-      bc = cok ? g.bias[col] : 0.0f;
+    // every wave, unconditionally, at clamped addresses (values of rows / columns outside
+    // the tile are never stored): a load under a branch makes the compiler's vmcnt for the
+    // prologue's own loads count the branch-free path, i.e. wait for the weights too
+    const int cc = min(col, g.N - 1);
+    swc = g.sw[cc];
+    bc = g.bias[cc];
+    if constexpr (resid) {
 #pragma unroll
       for (int i = 0; i < MF; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int r = 16 * i + 4 * fg + e, row = m0 + r;
-          rv[i][e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
+          const int row = min(m0 + 16 * i + 4 * fg + e, g.M - 1);
+          rv[i][e] = g.res[(long)row * g.ldr + cc];
         }
     }
   };
@@ -215,7 +228,11 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       const v4i afr = *reinterpret_cast<const v4i*>(As + (16 * i + fr) * LDA + k);
+#if defined(QTX_ABL) && (QTX_ABL & 4)   // diagnostic builds only: no matrix work
+      acc[i] += afr ^ bfr;
+#else
       acc[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, bfr, acc[i], 0, 0, 0);
+#endif
     }
   }
 
