@@ -23,6 +23,8 @@
 // position L = (0 + e[L]) + e[L+64], then a 64-position xor butterfly) maps onto this
 // layout as: L = 16 kt + 4 e + fg, so bits 0-1 are the lane xor 16 / xor 32 levels, bits
 // 2-3 in-lane (e), bits 4-5 in-lane (kt).  Keys <= 128.
+#include <cstdlib>
+
 #include "qtx_common.h"
 #include "qtx_kernels.h"
 
@@ -266,6 +268,7 @@ __device__ __forceinline__ void dma16_lds(const void* gsrc, const void* lds_dst)
                : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
 }
 
+template <bool PIPE>
 __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, float* sctx, int kp) {
   __shared__ __attribute__((aligned(16))) uint8_t Ks[AM_MAXK * 512];
   __shared__ __attribute__((aligned(16))) uint8_t Vs[AM_MAXK * 512];
@@ -321,19 +324,16 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) ctx[h][dt] = v4f{0, 0, 0, 0};
 
-  // the head loop is unrolled by instantiation (ctx[h] must be register-resident: a
-  // run-time head index would put the 128 accumulators in scratch)
-  static_for<8>([&](auto hc) {
+  // scores + softmax + P quantization of head h into x (the canonical trees of
+  // k_attn_mfma), and PV of head h from x into ctx[h]; FULL: all 128 keys present (no
+  // per-chunk tests, so the two phases of a pipelined iteration share one basic block)
+  auto scores_softmax = [&](auto hc, const v4i qcur, float (&x)[8][4], auto fullc) {
     constexpr int h = decltype(hc)::value;
-    __builtin_amdgcn_sched_barrier(0);
-    if (h == 0) QTX_STAMP(4);
-    const v4i qcur = qf;
-    if (h < 7) qf = *reinterpret_cast<const v4i*>(qbase + 64 * (h + 1));   // next head
+    constexpr bool FULL = decltype(fullc)::value;
     // ---- scores S^T: C[staged row 4fg + e = key 16kt + 4e + fg][query fr] --------------
-    float x[8][4];
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt) {
-      if (16 * kt < Sk) {
+      if (FULL || 16 * kt < Sk) {
         const int krow = kt * 16 + fr;
         const v4i kf = *reinterpret_cast<const v4i*>(Ks + krow * 512 + 16 * ((4 * h + fg) ^ fr));
         const v4i sc4 = __builtin_amdgcn_mfma_i32_16x16x64_i8(kf, qcur, v4i{0, 0, 0, 0}, 0, 0, 0);
@@ -349,7 +349,6 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
         for (int e = 0; e < 4; ++e) x[kt][e] = -3.0e38f;
       }
     }
-    if (h == 0) QTX_STAMP(5);
     // ---- softmax of row fr over its key slots (32 in the lane, 4 lanes), the canonical
     // trees of k_attn_mfma.  Absent keys: qexp(-3e38 - m) == 0 exactly.
     float m = x[0][0];
@@ -381,16 +380,18 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         x[kt][e] = div_cr(rintf(div_cr(x[kt][e], den, rden) * 127.0f), 127.0f, r127);
-    __builtin_amdgcn_sched_barrier(0);
-    if (h == 0) QTX_STAMP(6);
-    // ---- PV: A = P[row fr][k = 4 s4 + fg], B[k][n] = float(v[k][64h + 4n + dt]) * s_v[k] --
+  };
+  // ---- PV: A = P[row fr][k = 4 s4 + fg], B[k][n] = float(v[k][64h + 4n + dt]) * s_v[k] --
+  // in chunks of 32 keys (the V operand reads of a chunk are issued ahead of its MFMAs);
+  // padded keys of a chunk have P == 0 and s_v == 0, so their steps add +0 to a
+  // nonzero-or-+0 accumulator: exact
+  auto pv = [&](auto hc, const float (&x)[8][4], auto fullc) {
+    constexpr int h = decltype(hc)::value;
+    constexpr bool FULL = decltype(fullc)::value;
     const uint8_t* vrow = Vs + fg * 512 + 16 * ((4 * h + (fr >> 2)) ^ (4 * (fg & 1))) + 4 * (fr & 3);
-    // in chunks of 32 keys with no branch inside (the V operand reads of a chunk are
-    // issued ahead of its MFMAs); padded keys of a chunk have P == 0 and s_v == 0, so
-    // their steps add +0 to a nonzero-or-+0 accumulator: exact
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      if (32 * c < Sk) {
+      if (FULL || 32 * c < Sk) {
 #pragma unroll
         for (int s4 = 8 * c; s4 < 8 * c + 8; ++s4) {
           const float pa = x[s4 >> 2][s4 & 3];
@@ -404,8 +405,45 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
         }
       }
     }
-    if (h == 0) QTX_STAMP(7);
-  });
+  };
+  using full_t = std::integral_constant<bool, true>;
+  using part_t = std::integral_constant<bool, false>;
+  if constexpr (!PIPE) {
+    // the head loop is unrolled by instantiation (ctx[h] must be register-resident: a
+    // run-time head index would put the 128 accumulators in scratch)
+    static_for<8>([&](auto hc) {
+      constexpr int h = decltype(hc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      const v4i qcur = qf;
+      if (h < 7) qf = *reinterpret_cast<const v4i*>(qbase + 64 * (h + 1));   // next head
+      float x[8][4];
+      scores_softmax(hc, qcur, x, part_t{});
+      __builtin_amdgcn_sched_barrier(0);
+      pv(hc, x, part_t{});
+    });
+  } else {
+    // all 128 keys present: software pipelined — iteration h runs the scores and softmax
+    // of head h (VALU-bound) and the PV of head h-1 (f32 MFMA-bound) in one basic block,
+    // so the compiler interleaves the two (measured unpipelined: no overlap)
+    float xp[8][4];
+    static_for<9>([&](auto hc) {
+      constexpr int h = decltype(hc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      float xn[8][4];
+      if constexpr (h < 8) {
+        const v4i qcur = qf;
+        if (h < 7) qf = *reinterpret_cast<const v4i*>(qbase + 64 * (h + 1));   // next head
+        scores_softmax(std::integral_constant<int, (h < 8 ? h : 0)>{}, qcur, xn, full_t{});
+      }
+      if constexpr (h >= 1) pv(std::integral_constant<int, (h >= 1 ? h - 1 : 0)>{}, xp, full_t{});
+      if constexpr (h < 8) {
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) xp[kt][e] = xn[kt][e];
+      }
+    });
+  }
   QTX_STAMP(2);
 
   // ---- per-token quantization of the context rows 4fg + e (dims 64h + 4fr + dt):
@@ -464,7 +502,16 @@ hipError_t launch_attention_encq(const AttnArgs& a, int8_t* ctx8, float* sctx, h
   if (a.B < 128 && !force_encq) return hipErrorNotSupported;   // one workgroup per sentence:
   // below ~128 sentences the per-(head, query block) kernel spreads over more CUs
   if (kp && a.c_ld != 512) return hipErrorInvalidValue;
-  k_attn_encq<<<dim3(a.B), dim3(512), 0, st>>>(a, ctx8, sctx, kp ? 1 : 0);
+  // all keys present and unmasked positions only differ through kadd/sks: the pipelined
+  // head loop (QTX_ENCQ_NOPIPE=1: the sequential one, A/B)
+  static const bool nopipe = [] {
+    const char* v = getenv("QTX_ENCQ_NOPIPE");
+    return v && *v && *v != '0';
+  }();
+  if (a.Sk == AM_MAXK && !nopipe)
+    k_attn_encq<true><<<dim3(a.B), dim3(512), 0, st>>>(a, ctx8, sctx, kp ? 1 : 0);
+  else
+    k_attn_encq<false><<<dim3(a.B), dim3(512), 0, st>>>(a, ctx8, sctx, kp ? 1 : 0);
   return hipGetLastError();
 }
 
