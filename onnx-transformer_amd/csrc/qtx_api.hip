@@ -232,7 +232,7 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
         for (QLin* L : {&e.qkv, &e.o, &e.w1, &e.w2}) L->qkp = ar.take<int8_t>((size_t)L->N * L->K);
     if (c.weight_bits == 8 && c.d_ff % 512 == 0)   // weight-stationary copies (K = 512 GEMMs)
       for (auto& e : m->enc)
-        for (QLin* L : {&e.qkv, &e.w1}) L->qws = ar.take<int8_t>((size_t)L->N * L->K);
+        for (QLin* L : {&e.qkv, &e.o, &e.w1}) L->qws = ar.take<int8_t>((size_t)L->N * L->K);
     for (auto& d : m->dec) {
       lin(d.qkv, 3 * D, D); lin(d.o, D, D); lin(d.cq, D, D); lin(d.ckv, 2 * D, D);
       lin(d.co, D, D); lin(d.w1, F, D); lin(d.w2, D, F);
@@ -515,17 +515,28 @@ bool row_path(const qtx_config& c) {
 // With kp, a K = 512 GEMM over many rows runs weight-stationary (kp = 2, W from L.qws):
 // each workgroup keeps a 512-column slice of W on chip (qtx_wsgemm.hip); below ws_min_m
 // rows the per-workgroup W load is not amortized and the row GEMM is faster.
+// Measured (tools/enc_small.py, the greedy decode's encoder): at M = 2304 (B = 32, S = 72)
+// the Q/K/V and FFN1 launches on the weight-stationary kernel took the encoder 0.83 ->
+// 0.73 ms (the row GEMM's 128-row tiles give 18 workgroups).  The O-projection's residual +
+// LayerNorm epilogue runs weight-stationary only between ws_res_min_m and ws_res_max_m
+// (above it the KP row GEMM is faster).  QTX_WS_MIN_M / QTX_WS_RES_MIN_M / _MAX_M: A/B.
+long env_long(const char* name, long def) {
+  const char* e = getenv(name);
+  return e && *e ? atol(e) : def;
+}
 long ws_min_m() {
-  static const long v = [] {
-    const char* e = getenv("QTX_WS_MIN_M");
-    return e ? atol(e) : 8192L;
-  }();
+  static const long v = env_long("QTX_WS_MIN_M", 2048L);
   return v;
+}
+bool ws_res_ok(long M) {
+  static const long lo = env_long("QTX_WS_RES_MIN_M", 2048L), hi = env_long("QTX_WS_RES_MAX_M", 8192L);
+  return M >= lo && M < hi;
 }
 RowGemmArgs rowgemm(const QLin& L, const int8_t* a8, const float* sa, int M, int epi,
                     bool kp = false) {
   RowGemmArgs g{};
-  const bool ws = kp && L.qws && L.K == 512 && M >= ws_min_m();
+  const bool ws = kp && L.qws && L.K == 512 &&
+                  (epi == RE_RES_LN ? ws_res_ok(M) : M >= ws_min_m());
   g.A = a8; g.lda = L.K; g.sa = sa; g.W = ws ? L.qws : kp ? L.qkp : L.q; g.ldw = L.K;
   g.sw = L.s; g.bias = L.b;
   g.M = M; g.N = L.N; g.K = L.K; g.epi = epi; g.kp = ws ? 2 : kp;

@@ -1,0 +1,21 @@
+"""Three cfg2 greedy decodes (B=32, S=72) — for rocprofv3 kernel stats of the decode alone."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+_R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [_R, os.path.join(_R, "onnx-transformer_amd")]
+import bench  # noqa: E402
+from qtx.model import QtxModel  # noqa: E402
+from qtx.weights import ModelConfig, synthetic_state_dict  # noqa: E402
+
+m = QtxModel(synthetic_state_dict(20241223), ModelConfig())
+src, _ = bench.make_src(np.random.default_rng(1000), 32, 72)
+srcd = torch.from_numpy(src).cuda()
+mk = (srcd != 2).to(torch.uint8)
+ids = torch.empty((32, 72), dtype=torch.int64, device="cuda")
+for _ in range(3):
+    m.greedy(srcd, mk, max_len=72, start=0, out=ids)
+torch.cuda.synchronize()
