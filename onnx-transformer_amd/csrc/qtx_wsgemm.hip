@@ -420,13 +420,14 @@ constexpr int WP_R = 32, WP_STAGE = WP_R * WS_K;    // 16 KB A stage
 constexpr int WAIT_VM(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70 | 0xF00; }
 constexpr int WAIT_LGKM0 = 0xC07F;
 
-template <int EPI>
+template <int EPI, int SR = WS_SR>   // SR: K steps of W in registers (8: all of W, no LDS part)
 __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
+  constexpr int WL = 8 * (8 - SR) * 4 * 1024;      // W's LDS part
   // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias of the slice (4 KB) |
   // partial row maxima [8][32] (1 KB)
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WS_WL + 4096 + 8 * WP_R * 4];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 8 * WP_R * 4];
   uint8_t* const wl = lds + 2 * WP_STAGE;
-  float* const swl = reinterpret_cast<float*>(wl + WS_WL);    // [512] sw, then [512] bias
+  float* const swl = reinterpret_cast<float*>(wl + WL);    // [512] sw, then [512] bias
   float* const red = swl + 1024;                               // [8][32]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int f = lane & 15, gq = lane >> 4;
@@ -456,15 +457,15 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
     }
   };
   issue(0);
-  v4i wr[WS_SR][4];
+  v4i wr[SR][4];
   {
     const int8_t* wsrc = g.W + ((long)(t * 8 + wave) << 15);
 #pragma unroll
-    for (int p = 0; p < (8 - WS_SR) * 4; ++p)
-      dma16(wsrc + ((WS_SR * 4 + p) << 10) + lane * 16, wl + ((wave * (8 - WS_SR) * 4 + p) << 10));
+    for (int p = 0; p < (8 - SR) * 4; ++p)
+      dma16(wsrc + ((SR * 4 + p) << 10) + lane * 16, wl + ((wave * (8 - SR) * 4 + p) << 10));
     const v4i* ws = reinterpret_cast<const v4i*>(wsrc) + lane;
 #pragma unroll
-    for (int s = 0; s < WS_SR; ++s)
+    for (int s = 0; s < SR; ++s)
 #pragma unroll
       for (int j = 0; j < 4; ++j) wr[s][j] = ws[(s * 4 + j) * 64];
     // sw / bias of the slice into LDS (wave w: 128 floats)
@@ -474,7 +475,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
       *reinterpret_cast<float2*>(swl + 512 + c) = *reinterpret_cast<const float2*>(g.bias + 512 * t + c);
     }
 #pragma unroll
-    for (int s = 0; s < WS_SR; ++s)
+    for (int s = 0; s < SR; ++s)
 #pragma unroll
       for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(wr[s][j]));
   }
@@ -506,8 +507,8 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
       for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const v4i*>(cur + ((s * 2 + i) << 10) + lane * 16);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        b[j] = s < WS_SR ? wr[s < WS_SR ? s : 0][j]
-                         : *reinterpret_cast<const v4i*>(wl + (((wave * (8 - WS_SR) + s - WS_SR) * 4 + j) << 10) + lane * 16);
+        b[j] = s < SR ? wr[s < SR ? s : 0][j]
+                         : *reinterpret_cast<const v4i*>(wl + (((wave * (8 - SR) + s - SR) * 4 + j) << 10) + lane * 16);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -691,7 +692,12 @@ hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {
     const dim3 grid(nsl * wpt), block(512);
     switch (g.epi) {
       case RE_QUANT: k_gemm_wsp<RE_QUANT><<<grid, block, 0, st>>>(g); break;
-      case RE_RELU_PMAX: k_gemm_wsp<RE_RELU_PMAX><<<grid, block, 0, st>>>(g); break;
+      case RE_RELU_PMAX:
+        // the row-max pass has a light epilogue: all of W fits in registers (no W reads
+        // from LDS in the main loop); QTX_WSP_PMAX_SR=5: the LDS-split variant (A/B)
+        if (getenv_flag("QTX_WSP_PMAX_SR5")) k_gemm_wsp<RE_RELU_PMAX><<<grid, block, 0, st>>>(g);
+        else k_gemm_wsp<RE_RELU_PMAX, 8><<<grid, block, 0, st>>>(g);
+        break;
       default: k_gemm_wsp<RE_RELU_QUANT_PMAX><<<grid, block, 0, st>>>(g); break;
     }
     return hipGetLastError();
