@@ -567,10 +567,26 @@ int row_res_ln(const QLin& L, const int8_t* a8, const float* sa, int M, float* x
 }
 // FFN1: relu(a8 . W1^T) quantized per token over all d_ff columns, two passes (row
 // maxima, then recompute + quantize: cheaper than the fp32 hidden's round trip)
+// FFN1 in one weight-stationary pass with the row maxima exchanged between the column
+// slices' workgroups inside the launch (k_gemm_wsx); QTX_NO_WSX=1: the two passes
+bool wsx_on() {
+  static const bool v = [] {
+    const char* e = getenv("QTX_NO_WSX");
+    return !(e && *e && *e != '0');
+  }();
+  return v;
+}
 int row_ffn1(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa, int M,
              Scratch& s, hipStream_t st,
              const FaultArgs& fa = FaultArgs{}, bool kp = false) {
   RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RELU_PMAX, kp);
+  if (g.kp == 2 && L.N == 2048 && fa.kind == FK_NONE && wsx_on()) {
+    g.epi = RE_RELU_QUANT_PMAX;
+    g.pmax_out = s.y;                // granules: 32 * M bytes of the (unused) fp32 GEMM scratch
+    g.out8 = s.h8; g.ldo8 = c.d_ff; g.os = s.sh;
+    HIPCHK(launch_gemm_wsx(g, st));
+    return QTX_OK;
+  }
   g.fault = fa;
   g.pmax_out = s.pmax;
   HIPCHK(launch_row_gemm_any(g, st));
@@ -834,7 +850,10 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
 // streams, the second half one kernel behind, so the HBM-bound epilogues (residual +
 // LayerNorm) of one half overlap the MFMA / VALU-bound kernels (attention, FFN) of the
 // other on different CUs.  Results are identical (rows are independent).
-bool enc_split(int B) { return B >= 256 && !getenv("QTX_ENC_NOSPLIT"); }
+// (not with the one-pass FFN1: its workgroups wait for their partner slices, which two
+// concurrent launches on two streams could keep from ever being resident together)
+bool wsx_on();
+bool enc_split(int B) { return B >= 256 && !getenv("QTX_ENC_NOSPLIT") && !wsx_on(); }
 
 size_t enc_ws(const qtx_config& c, int B, int S) {
   Arena ar;

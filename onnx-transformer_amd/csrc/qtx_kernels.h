@@ -150,6 +150,9 @@ hipError_t launch_gemm_row(const RowGemmArgs& a, hipStream_t st);
 // slice of W in registers and streams 64-row blocks of A (KP layout); W packed by
 // launch_pack_w_ws.  Same epilogues and outputs as launch_gemm_row(kp = 1); no faults.
 hipError_t launch_gemm_ws(const RowGemmArgs& a, hipStream_t st);
+// FFN1 in one pass (N = 2048, K = 512, WS weights, RE_RELU_QUANT_PMAX outputs): the slices'
+// row maxima exchanged in-launch through the u64 granule array in a.pmax_out (>= 32*M B)
+hipError_t launch_gemm_wsx(const RowGemmArgs& a, hipStream_t st);
 hipError_t launch_pack_w_ws(const int8_t* W, int N, int K, int8_t* out, hipStream_t st);
 
 hipError_t launch_gemm(const GemmArgs& a, int wbits, hipStream_t st);

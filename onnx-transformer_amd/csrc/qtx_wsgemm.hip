@@ -679,6 +679,259 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
   QTX_STAMP_VAL(6, nblk);
 }
 
+// =====================================================================================
+// k_gemm_wsx: FFN1 (N = 2048, K = 512) in ONE pass — ReLU + per-token quantization of the
+// hidden over all 2048 columns, without the row-max pre-pass (position_feed_forward.py:12,
+// quant_linear.py:30-43).  The 4 workgroups holding the 4 512-column slices of a row group
+// (one XCD under round-robin placement — speed only) exchange their partial row maxima
+// inside the launch: for each 32-row block a workgroup publishes its slice's row maxima as
+// data-tagged 8-byte granules {tag, value} (one write-through sc1 store each, the
+// MI355X_MICROARCH.md R2 hand-off: no flag, no fence) and reads the other three slices'
+// granules with sc1 loads.  The software pipeline is one block deeper than k_gemm_wsp:
+// iteration k issues block k's MFMAs, forms y and the slice maxima of block k-1 (published
+// at the end of the iteration) and quantizes block k-2, whose partner maxima were published
+// an iteration earlier — the hand-off latency hides under a whole iteration.
+// Requires all 4 slice workgroups of a row group resident together (grid <= 256, one
+// workgroup per CU); every spin is bounded (a timed-out block is quantized with its own
+// slice maximum: wrong, never hung — the parity tests would catch it).  The granule array
+// (4 x 32 x ceil(M/32) u64, in g.pmax_out) is zeroed before every launch.
+// =====================================================================================
+__global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
+  constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 8 * WP_R * 4];
+  uint8_t* const wl = lds + 2 * WP_STAGE;
+  float* const swl = reinterpret_cast<float*>(wl + WL);    // [512] sw, then [512] bias
+  float* const red = swl + 1024;                            // [8][32]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int f = lane & 15, gq = lane >> 4;
+  // XCD-grouped mapping: i = blockIdx / 8 within XCD blockIdx % 8; slice t = i % 4
+  const int ng = (gridDim.x >> 3) >> 2, i8 = blockIdx.x >> 3;
+  const int t = i8 & 3, r0 = (i8 >> 2) * 8 + (blockIdx.x & 7), wpt = 8 * ng;
+  const int nb = (g.M + WP_R - 1) / WP_R;
+  if (r0 >= nb) return;                         // the whole row group (all 4 slices) skips
+  const int nblk = (nb - r0 + wpt - 1) / wpt;
+  unsigned long long* const gran = reinterpret_cast<unsigned long long*>(g.pmax_out);
+
+  auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto rbk = [&](int k) { return r0 + min(k, nblk - 1) * wpt; };
+  auto issue = [&](int k) {
+    uint8_t* st = lds + (k & 1) * WP_STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long row = min(rbk(k) * WP_R + 16 * i + f, g.M - 1);
+      dma16(g.A + kp_off(row, 64 * wave + 16 * gq, WS_K), st + ((wave * 2 + i) << 10));
+    }
+  };
+  issue(0);
+  v4i wr[SR][4];
+  {
+    const int8_t* wsrc = g.W + ((long)(t * 8 + wave) << 15);
+#pragma unroll
+    for (int p = 0; p < (8 - SR) * 4; ++p)
+      dma16(wsrc + ((SR * 4 + p) << 10) + lane * 16, wl + ((wave * (8 - SR) * 4 + p) << 10));
+    const v4i* ws = reinterpret_cast<const v4i*>(wsrc) + lane;
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wr[s][j] = ws[(s * 4 + j) * 64];
+    if (wave < 4) {
+      const int c = 128 * wave + 2 * lane;
+      *reinterpret_cast<float2*>(swl + c) = *reinterpret_cast<const float2*>(g.sw + 512 * t + c);
+      *reinterpret_cast<float2*>(swl + 512 + c) = *reinterpret_cast<const float2*>(g.bias + 512 * t + c);
+    }
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(wr[s][j]));
+  }
+  const int cs = 64 * wave + 16 * gq;
+  const int c0 = 512 * t + cs;
+  const __amdgpu_buffer_rsrc_t orsrc = ws_rsrc(g.out8, (long)(g.M + (g.M & 1)) * g.ldo8);
+  const __amdgpu_buffer_rsrc_t srsrc = ws_rsrc(g.os, t == 0 ? 4L * g.M : 0L);
+
+  auto mfma_steps = [&](v4i (&acc)[2][4], const uint8_t* cur, int s0, int s1) {
+#pragma unroll
+    for (int s = s0; s < s1; ++s) {
+      v4i a[2], b[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const v4i*>(cur + ((s * 2 + i) << 10) + lane * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = s < SR ? wr[s < SR ? s : 0][j]
+                      : *reinterpret_cast<const v4i*>(wl + (((wave * (8 - SR) + s - SR) * 4 + j) << 10) + lane * 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+    }
+  };
+  // y = relu(((acc * sa) * sw) + b) of a block, and the wave's partial row maxima into red
+  auto form_y = [&](const v4i (&acc)[2][4], float sa, float (&y)[2][16]) {
+    float sr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      sr[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sa)));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 s4 = *reinterpret_cast<const float4*>(swl + cs + 4 * j);
+      const float4 b4 = *reinterpret_cast<const float4*>(swl + 512 + cs + 4 * j);
+      const float swj[4] = {s4.x, s4.y, s4.z, s4.w}, bj[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          y[i][4 * j + e] = fmaxf(((float)acc[i][j][e] * sr[i]) * swj[e] + bj[e], 0.0f);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float a = y[i][0];
+#pragma unroll
+      for (int c = 1; c < 16; ++c) a = fmaxf(a, y[i][c]);
+      a = fmaxf(a, __shfl_xor(a, 16));
+      a = fmaxf(a, __shfl_xor(a, 32));
+      red[wave * WP_R + 16 * i + f] = a;
+    }
+  };
+  // the slice's row maximum of row (lane & 31) over its 8 waves (after a barrier)
+  auto slice_max = [&]() {
+    float m = red[lane & 31];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w * WP_R + (lane & 31)]);
+    return m;
+  };
+  auto gidx = [&](int rb, int tt) { return ((long)rb * 4 + tt) * 32 + (lane & 31); };
+  auto publish = [&](int k, float m) {
+    if (wave == 0 && lane < 32)
+      __hip_atomic_store(gran + gidx(rbk(k), t), (1ull << 32) | __float_as_uint(m),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // the row maximum over all 4 slices: this slice's, then the partners' granules (bounded)
+  auto full_max = [&](int k, float mloc) {
+    const int rb = rbk(k);
+    float m = mloc;
+    for (unsigned spin = 0;; ++spin) {
+      bool ok = true;
+      float mx = mloc;
+#pragma unroll
+      for (int d = 1; d < 4; ++d) {
+        const unsigned long long v = __hip_atomic_load(gran + gidx(rb, (t + d) & 3), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        ok &= (v >> 32) == 1ull;
+        mx = fmaxf(mx, __uint_as_float((unsigned)v));
+      }
+      if (__all(ok)) { m = mx; break; }
+      if (spin > (1u << 18)) break;                 // bounded: never hang
+      __builtin_amdgcn_s_sleep(2);
+    }
+    return m;
+  };
+  auto quant_store = [&](int k, const float (&y)[2][16], float m) {
+    const int m0 = rbk(k) * WP_R;
+    const float sc = quant_scale(m, 127.0f);
+    const float kk = m < 0x1p37f ? 1.0f : 0x1p-64f;
+    const float scs = sc * kk, invs = 1.0f / scs;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc), srsrc, 4 * (m0 + (lane & 31)), 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int src = 4 * (16 * i + f);
+      const float b = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(scs)));
+      const float yi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(invs)));
+      const float k2 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(kk)));
+      uint32_t d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        d[j] = pack4_biased(rint_biased(div_cr(y[i][4 * j] * k2, b, yi)),
+                            rint_biased(div_cr(y[i][4 * j + 1] * k2, b, yi)),
+                            rint_biased(div_cr(y[i][4 * j + 2] * k2, b, yi)),
+                            rint_biased(div_cr(y[i][4 * j + 3] * k2, b, yi)));
+      const long row = m0 + 16 * i + f;
+      __builtin_amdgcn_raw_buffer_store_b128(v4u{d[0], d[1], d[2], d[3]}, orsrc, (int)kp_off(row, c0, g.ldo8), 0, 0);
+    }
+  };
+  auto zero = [](v4i (&acc)[2][4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+  };
+  auto sa_of = [&](int k) { return g.sa[min(rbk(k) * WP_R + (lane & 31), g.M - 1)]; };
+
+  // ---- block 0: main loop only
+  v4i accp[2][4];
+  float yq[2][16];                  // y of the block waiting for its partners' maxima
+  float mq = 0.0f;                  // ... and its own slice maximum
+  __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
+  __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+  __builtin_amdgcn_s_barrier();
+  float sap = sa_of(0);
+  issue(1);
+  zero(accp);
+  mfma_steps(accp, lds, 0, 8);
+  __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
+  // ---- steady state: iteration k: MFMAs of block k, y + maxima of block k-1 (published),
+  // quantization of block k-2
+  for (int k = 1; k <= nblk; ++k) {
+    // block k's DMA retired (behind it only the previous iteration's stores: 3 per wave
+    // plus wave 0's granule store — vmcnt(3) over-waits on wave 0, never under-waits)
+    __builtin_amdgcn_s_waitcnt(WAIT_VM(3));
+    __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+    __builtin_amdgcn_s_barrier();
+    const bool more = k < nblk;     // block k exists (uniform)
+    asm volatile("" ::"v"(sap));
+    float sac = more ? sa_of(k) : 0.0f;
+    if (more) issue(k + 1);
+    const uint8_t* cur = lds + (k & 1) * WP_STAGE;
+    v4i acc[2][4];
+    zero(acc);
+    float y[2][16];
+    if (more) mfma_steps(acc, cur, 0, 4);
+    form_y(accp, sap, y);           // block k-1
+    __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+    __builtin_amdgcn_s_barrier();
+    const float mloc = slice_max(); // block k-1's slice maximum (red complete)
+    float m2 = 0.0f;
+    if (k >= 2) m2 = full_max(k - 2, mq);
+    if (more) mfma_steps(acc, cur, 4, 8);
+    if (k >= 2) quant_store(k - 2, yq, m2);
+    publish(k - 1, mloc);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) accp[i][j] = acc[i][j];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int c = 0; c < 16; ++c) yq[i][c] = y[i][c];
+    mq = mloc;
+    sap = sac;
+  }
+  // ---- the last block: its partners' maxima, then its quantization
+  quant_store(nblk - 1, yq, full_max(nblk - 1, mq));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+hipError_t launch_gemm_wsx(const RowGemmArgs& g, hipStream_t st) {
+  if (g.M <= 0) return hipSuccess;
+  if (g.K != WS_K || g.N != 2048 || g.epi != RE_RELU_QUANT_PMAX || g.fault.kind != FK_NONE ||
+      !g.pmax_out || !g.out8 || !g.os)
+    return hipErrorInvalidValue;
+  const int nb = (g.M + WP_R - 1) / WP_R;
+  int ng = 8;                                 // row groups per XCD (4 slices each: 32 WGs)
+  if (8 * ng > nb) ng = (nb + 7) / 8;
+  const long ngran = 4L * 32 * nb;            // u64 granules, zeroed before every launch
+  hipError_t e = hipMemsetAsync(g.pmax_out, 0, (size_t)ngran * 8, st);
+  if (e != hipSuccess) return e;
+  k_gemm_wsx<<<dim3(8 * 4 * ng), dim3(512), 0, st>>>(g);
+  return hipGetLastError();
+}
+
 hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return hipSuccess;
   if (g.K != WS_K || g.N % 512 || g.N <= 0 || (g.epi == RE_RES_LN && g.N != 512) ||
