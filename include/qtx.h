@@ -248,7 +248,11 @@ typedef struct qtx_row_gemm {
    * kp = 2: the weight-stationary kernel (K == 512 only): A in the KP layout, W packed by
    * qtx_pack_w_ws; each workgroup keeps a 512-column slice of W on chip and streams 64-row
    * blocks of A.  Outputs exactly as kp = 1, except that epi 3's out8 must hold M + (M & 1)
-   * rows (the KP pad row of an odd M is written as scratch). */
+   * rows (the KP pad row of an odd M is written as scratch).
+   * kp = 3: epi 3 in ONE pass (N == 2048, K == 512, W as for kp = 2): the per-token row
+   * maximum is exchanged between the column slices' workgroups inside the launch, so
+   * pmax_in / pmax_n are not read; pmax_out is the exchange scratch (>= 32 * M + 1024 bytes,
+   * overwritten).  The encoder's FFN1 (qtx_encoder_forward at M >= 2048). */
   int32_t kp;
 } qtx_row_gemm;
 int32_t qtx_linear_rows(const qtx_row_gemm* args, void* stream);

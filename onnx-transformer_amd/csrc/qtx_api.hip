@@ -1582,10 +1582,12 @@ int32_t qtx_linear_rows(const qtx_row_gemm* a, void* stream) {
                   (g.epi == RE_RES_LN && g.res && g.xout && g.ln_a && g.ln_b &&
                    (g.lnq ? g.lns != nullptr : g.lnout != nullptr)) ||
                   (g.epi == RE_RELU_PMAX && g.pmax_out) ||
-                  (g.epi == RE_RELU_QUANT_PMAX && g.out8 && g.os && g.pmax_in && g.pmax_n > 0);
+                  (g.epi == RE_RELU_QUANT_PMAX && g.out8 && g.os &&
+                   (g.kp == 3 ? g.pmax_out != nullptr : (g.pmax_in && g.pmax_n > 0)));
   if (!ok) return fail(QTX_E_INVALID, "operands missing for epi %d", g.epi);
-  const hipError_t e = g.kp == 2 ? launch_gemm_ws(g, (hipStream_t)stream)
-                                  : launch_gemm_row(g, (hipStream_t)stream);
+  const hipError_t e = g.kp == 3   ? launch_gemm_wsx(g, (hipStream_t)stream)
+                       : g.kp == 2 ? launch_gemm_ws(g, (hipStream_t)stream)
+                                   : launch_gemm_row(g, (hipStream_t)stream);
   if (e == hipErrorInvalidValue)
     return fail(QTX_E_UNSUPPORTED, "rows GEMM: N=%d K=%d epi=%d kp=%d", g.N, g.K, g.epi, g.kp);
   HIPCHK(e);

@@ -452,6 +452,14 @@ def test_linear_rows_ws(torch, oracle_model, monkeypatch, M, nopipe):
     qh, s = O.quant_rows(h)
     np.testing.assert_array_equal(_from_kp(h8.cpu().numpy(), M), qh)
     np.testing.assert_array_equal(sh.cpu().numpy(), s)
+    # kp = 3: the same hidden in ONE pass (row maxima exchanged between the column slices'
+    # workgroups inside the launch; pmax_in unused, pmax_out = exchange scratch)
+    h8b = torch.zeros_like(h8)
+    shb = torch.full((M,), -1.0, dtype=torch.float32, device="cuda")
+    gx = torch.empty(((32 * M + 1024) // 4,), dtype=torch.float32, device="cuda")
+    _rows_call(torch, **{**base, "kp": 3}, epi=3, pmax_out=gx, out8=h8b, ldo8=2048, os=shb)
+    np.testing.assert_array_equal(_from_kp(h8b.cpu().numpy(), M), qh)
+    np.testing.assert_array_equal(shb.cpu().numpy(), s)
     # epi 1 (O-proj), next LayerNorm quantized KP, then the fp32 LayerNorm output variant
     qw, sw, wk, b = weights(512)
     res = (rng.standard_normal((M, 512)) * 2).astype(f32)
