@@ -32,6 +32,8 @@
 #include "qtx_kernels.h"
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 QTX_STAMP_SETTER(ws)
 
@@ -926,10 +928,29 @@ hipError_t launch_gemm_wsx(const RowGemmArgs& g, hipStream_t st) {
   int ng = 8;                                 // row groups per XCD (4 slices each: 32 WGs)
   if (8 * ng > nb) ng = (nb + 7) / 8;
   const long ngran = 4L * 32 * nb;            // u64 granules, zeroed before every launch
-  hipError_t e = hipMemsetAsync(g.pmax_out, 0, (size_t)ngran * 8, st);
+  // Two of these launches running at once (two threads' streams) could each hold CUs that
+  // the other's waiting partner workgroups need: launches are serialized per device through
+  // an event (a stream waits for the previous launch, whatever stream it ran on).  Other
+  // kernels never wait on anything, so sharing the GPU with them only delays the partners.
+  static std::mutex mu;
+  static std::map<int, hipEvent_t> last;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  e = hipStreamIsCapturing(st, &cap);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lock(mu);
+  hipEvent_t& ev = last[dev];
+  if (cap == hipStreamCaptureStatusNone) {
+    if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(st, ev, 0)) != hipSuccess) return e;
+  }
+  if ((e = hipMemsetAsync(g.pmax_out, 0, (size_t)ngran * 8, st)) != hipSuccess) return e;
   k_gemm_wsx<<<dim3(8 * 4 * ng), dim3(512), 0, st>>>(g);
-  return hipGetLastError();
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (cap == hipStreamCaptureStatusNone) return hipEventRecord(ev, st);
+  return hipSuccess;
 }
 
 hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {

@@ -21,17 +21,20 @@ B = int(os.environ.get("QTX_CHAIN_B", "32"))
 N_LAUNCH = 50
 
 
+NLAYER = int(os.environ.get("QTX_CHAIN_LAYERS", "1"))   # distinct weight sets cycled (6: as the decode)
+
+
 def chain_us(fn):
     for _ in range(3):
-        fn(C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        fn(C.c_void_p(torch.cuda.current_stream().cuda_stream), 0)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
             st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-            for _ in range(N_LAUNCH):
-                fn(st)
+            for i in range(N_LAUNCH):
+                fn(st, i % NLAYER)
     for _ in range(3):
         g.replay()
     torch.cuda.synchronize()
@@ -54,7 +57,11 @@ step = T(np.array([40, 0, 0, 0], np.int32))
 mask = T(np.ones((B, 72), np.uint8))
 x = T(rng.standard_normal((B, 512)).astype(np.float32))
 h = T(np.abs(rng.standard_normal((B, 2048))).astype(np.float32))
-W = {nk: T(rng.integers(-127, 128, nk).astype(np.int8)) for nk in [(1536, 512), (512, 512), (2048, 512), (512, 2048)]}
+WL = [{nk: T(rng.integers(-127, 128, nk).astype(np.int8)) for nk in [(1536, 512), (512, 512), (2048, 512), (512, 2048)]}
+      for _ in range(NLAYER)]
+W = WL[0]
+KVL = [(T(rng.integers(-127, 128, (B, 72, 512)).astype(np.int8)), T(rng.integers(-127, 128, (B, 72, 512)).astype(np.int8)))
+       for _ in range(NLAYER)]
 sw = T(np.full(2048, 0.01, np.float32))
 bias = T(np.zeros(2048, np.float32))
 out = torch.empty((B, 2048), device="cuda")
@@ -68,19 +75,19 @@ Z = C.c_void_p(0)
 
 
 def skinny(amode, X, ldx, pin, pn, w, N, K, flags, r=None, pout=None):
-    return lambda st: _lib.call("qtx_skinny_linear", amode, Z, Z, P(X), ldx, P(lna), P(lnb), P(pin), pn,
-                                P(w), P(sw), P(bias), B, N, K, 8, flags, P(r), P(out), P(pout), st)
+    return lambda st, l: _lib.call("qtx_skinny_linear", amode, Z, Z, P(X), ldx, P(lna), P(lnb), P(pin), pn,
+                                   P(WL[l][(N, K)]), P(sw), P(bias), B, N, K, 8, flags, P(r), P(out), P(pout), st)
 
 
 cases = {
     "LN+QKV   (A_LN, N=1536)": skinny(1, x, 512, None, 0, W[(1536, 512)], 1536, 512, 0),
-    "self-attn (k_dec_attn, 41 keys)": lambda st: _lib.call(
-        "qtx_decode_attention", 1, P(y), 1536, P(kc), P(vc), P(skc), P(svc), 72, P(step), 0, Z, B,
+    "self-attn (k_dec_attn, 41 keys)": lambda st, l: _lib.call(
+        "qtx_decode_attention", 1, P(y), 1536, P(KVL[l][0]), P(KVL[l][1]), P(skc), P(svc), 72, P(step), 0, Z, B,
         P(ctx), P(pma), st),
     "O+res    (A_F32Q, K=512)": skinny(2, ctx, 512, pma, 8, W[(512, 512)], 512, 512, 2, res),
     "LN+Qc    (A_LN, N=512)": skinny(1, x, 512, None, 0, W[(512, 512)], 512, 512, 0),
-    "cross-attn (72 keys)": lambda st: _lib.call(
-        "qtx_decode_attention", 0, P(y), 512, P(kc), P(vc), P(skc), P(svc), 72, Z, 72, P(mask), B,
+    "cross-attn (72 keys)": lambda st, l: _lib.call(
+        "qtx_decode_attention", 0, P(y), 512, P(KVL[l][0]), P(KVL[l][1]), P(skc), P(svc), 72, Z, 72, P(mask), B,
         P(ctx), P(pma), st),
     "LN+FFN1  (A_LN, N=2048, relu+rowmax)": skinny(1, x, 512, None, 0, W[(2048, 512)], 2048, 512, 5, None, pm_out),
     "FFN2+res (A_F32Q, K=2048)": skinny(2, h, 2048, pmf, 128, W[(512, 2048)], 512, 2048, 2, res),
@@ -92,3 +99,22 @@ for name, fn in cases.items():
     print(f"B={B} {name:40s} {t:6.2f} us/launch", flush=True)
 print(f"B={B} one decoder layer (8 launches, attention counted as listed): {tot + 0:.1f} us "
       f"(the cross-attn/O pair appears twice per layer: + {0:.1f})", flush=True)
+
+# the 8 kernels of a decoder layer in the decode step's order, back to back (different code
+# and data every launch, as in the real step) vs the sum of their single-kernel chains
+order = ["LN+QKV   (A_LN, N=1536)", "self-attn (k_dec_attn, 41 keys)", "O+res    (A_F32Q, K=512)",
+         "LN+Qc    (A_LN, N=512)", "cross-attn (72 keys)", "O+res    (A_F32Q, K=512)",
+         "LN+FFN1  (A_LN, N=2048, relu+rowmax)", "FFN2+res (A_F32Q, K=2048)"]
+fns = [cases[k] for k in order]
+
+
+def layer_seq(st, l):
+    for f in fns:
+        f(st, l)
+
+
+N_LAUNCH_SAVE = N_LAUNCH
+N_LAUNCH = 12
+t_layer = chain_us(layer_seq) * 1  # us per layer_seq call = per layer
+print(f"B={B} decoder layer as the step's 8-kernel sequence: {t_layer:.1f} us "
+      f"(sum of the single-kernel chains {tot + 2.6:.1f} us incl. the Oc twin)", flush=True)
