@@ -166,7 +166,7 @@ def time_row_gemms(M=256 * 128, reps=10, ws=True, operands="encoder"):
     x = torch.randn((M, D), device="cuda")
     lna, lnb = torch.ones(D, device="cuda"), torch.zeros(D, device="cuda")
     pm = torch.full((4, M), 3.0, device="cuda")
-    gx = torch.empty((32 * M + 1024) // 4, device="cuda")
+    gx = torch.empty((32 * M + 2048) // 4, device="cuda")
     # the encoder runs the KP instances (csrc/qtx_api.hip encoder_run: kp = 1): weights
     # packed by qtx_pack_w_kp, A in the KP layout (random bytes: any layout of them is)
     kps = {}

@@ -251,7 +251,7 @@ typedef struct qtx_row_gemm {
    * rows (the KP pad row of an odd M is written as scratch).
    * kp = 3: epi 3 in ONE pass (N == 2048, K == 512, W as for kp = 2): the per-token row
    * maximum is exchanged between the column slices' workgroups inside the launch, so
-   * pmax_in / pmax_n are not read; pmax_out is the exchange scratch (>= 32 * M + 1024 bytes,
+   * pmax_in / pmax_n are not read; pmax_out is the exchange scratch (>= 32 * M + 2048 bytes,
    * overwritten).  The encoder's FFN1 (qtx_encoder_forward at M >= 2048). */
   int32_t kp;
 } qtx_row_gemm;

@@ -582,7 +582,7 @@ int row_ffn1(const qtx_config& c, const QLin& L, const int8_t* a8, const float* 
   RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RELU_PMAX, kp);
   if (g.kp == 2 && L.N == 2048 && fa.kind == FK_NONE && wsx_on()) {
     g.epi = RE_RELU_QUANT_PMAX;
-    g.pmax_out = s.y;                // granules: 32 * M bytes of the (unused) fp32 GEMM scratch
+    g.pmax_out = s.y;                // granules + ticket: <= 32 * M + 2048 bytes of the (unused) fp32 GEMM scratch
     g.out8 = s.h8; g.ldo8 = c.d_ff; g.os = s.sh;
     HIPCHK(launch_gemm_wsx(g, st));
     return QTX_OK;

@@ -32,8 +32,6 @@
 #include "qtx_kernels.h"
 
 #include <cstdlib>
-#include <map>
-#include <mutex>
 
 QTX_STAMP_SETTER(ws)
 
@@ -693,10 +691,12 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
 // iteration k issues block k's MFMAs, forms y and the slice maxima of block k-1 (published
 // at the end of the iteration) and quantizes block k-2, whose partner maxima were published
 // an iteration earlier — the hand-off latency hides under a whole iteration.
-// Requires all 4 slice workgroups of a row group resident together (grid <= 256, one
-// workgroup per CU); every spin is bounded (a timed-out block is quantized with its own
-// slice maximum: wrong, never hung — the parity tests would catch it).  The granule array
-// (4 x 32 x ceil(M/32) u64, in g.pmax_out) is zeroed before every launch.
+// Work is assigned by arrival ticket (below), so a row group only waits for partners that
+// have started or will start once other groups finish: no co-residency assumption, safe
+// beside any other launch.  Every spin is still bounded (a timed-out block would be
+// quantized with its own slice maximum: wrong, never hung — the parity tests catch it).
+// The granule array (4 x 32 x ceil(M/32) u64 + the ticket counter, in g.pmax_out) is
+// zeroed before every launch.
 // =====================================================================================
 __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
   constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
@@ -706,13 +706,23 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
   float* const red = swl + 1024;                            // [8][32]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int f = lane & 15, gq = lane >> 4;
-  // XCD-grouped mapping: i = blockIdx / 8 within XCD blockIdx % 8; slice t = i % 4
-  const int ng = (gridDim.x >> 3) >> 2, i8 = blockIdx.x >> 3;
-  const int t = i8 & 3, r0 = (i8 >> 2) * 8 + (blockIdx.x & 7), wpt = 8 * ng;
+  // Work by arrival ticket, not blockIdx: the started workgroups always hold the lowest
+  // tickets, so groups whose 4 tickets have all started run to completion and free their
+  // CUs, whatever else shares the GPU (another launch of this kernel included): no
+  // co-residency assumption, no deadlock.  The ticket counter follows the granules.
   const int nb = (g.M + WP_R - 1) / WP_R;
+  unsigned long long* const gran = reinterpret_cast<unsigned long long*>(g.pmax_out);
+  __shared__ int ticket;
+  if (tid == 0)
+    ticket = (int)atomicAdd(reinterpret_cast<unsigned*>(gran + 4L * 32 * nb), 1u);
+  __syncthreads();
+  // slices of a row group at tickets 8 apart: workgroups start about in blockIdx order and
+  // are dealt round-robin to the 8 XCDs, so the 4 partners mostly share an XCD (speed only);
+  // a group is complete once its highest ticket has started (any 25 started tickets hold one)
+  const int q = ticket, wpt = gridDim.x >> 2;
+  const int t = (q >> 3) & 3, r0 = (q & 7) + 8 * (q >> 5);
   if (r0 >= nb) return;                         // the whole row group (all 4 slices) skips
   const int nblk = (nb - r0 + wpt - 1) / wpt;
-  unsigned long long* const gran = reinterpret_cast<unsigned long long*>(g.pmax_out);
 
   auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
     const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
@@ -880,8 +890,9 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
   // ---- steady state: iteration k: MFMAs of block k, y + maxima of block k-1 (published),
   // quantization of block k-2
   for (int k = 1; k <= nblk; ++k) {
-    // block k's DMA retired (behind it only the previous iteration's stores: 3 per wave
-    // plus wave 0's granule store — vmcnt(3) over-waits on wave 0, never under-waits)
+    // block k's DMA retired (behind it only the previous iteration's stores: 3 per wave —
+    // iteration 1, which quantizes nothing, issues 3 dropped ones — plus wave 0's granule
+    // store: vmcnt(3) over-waits on wave 0, never under-waits)
     __builtin_amdgcn_s_waitcnt(WAIT_VM(3));
     __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
     __builtin_amdgcn_s_barrier();
@@ -901,7 +912,13 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
     float m2 = 0.0f;
     if (k >= 2) m2 = full_max(k - 2, mq);
     if (more) mfma_steps(acc, cur, 4, 8);
-    if (k >= 2) quant_store(k - 2, yq, m2);
+    if (k >= 2) {
+      quant_store(k - 2, yq, m2);
+    } else {                        // the 3 stores the next top wait counts (range 0: dropped)
+      const __amdgpu_buffer_rsrc_t nul = ws_rsrc(g.out8, 0L);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) __builtin_amdgcn_raw_buffer_store_b32(0u, nul, 0, 0, 0);
+    }
     publish(k - 1, mloc);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -927,30 +944,13 @@ hipError_t launch_gemm_wsx(const RowGemmArgs& g, hipStream_t st) {
   const int nb = (g.M + WP_R - 1) / WP_R;
   int ng = 8;                                 // row groups per XCD (4 slices each: 32 WGs)
   if (8 * ng > nb) ng = (nb + 7) / 8;
-  const long ngran = 4L * 32 * nb;            // u64 granules, zeroed before every launch
-  // Two of these launches running at once (two threads' streams) could each hold CUs that
-  // the other's waiting partner workgroups need: launches are serialized per device through
-  // an event (a stream waits for the previous launch, whatever stream it ran on).  Other
-  // kernels never wait on anything, so sharing the GPU with them only delays the partners.
-  static std::mutex mu;
-  static std::map<int, hipEvent_t> last;
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
+  // u64 granules + the ticket counter (padded: a memset of a multiple of 16 bytes), zeroed
+  // before every launch
+  const long ngran = 4L * 32 * nb + 2;
+  hipError_t e = hipMemsetAsync(g.pmax_out, 0, (size_t)ngran * 8, st);
   if (e != hipSuccess) return e;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  e = hipStreamIsCapturing(st, &cap);
-  if (e != hipSuccess) return e;
-  std::lock_guard<std::mutex> lock(mu);
-  hipEvent_t& ev = last[dev];
-  if (cap == hipStreamCaptureStatusNone) {
-    if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(st, ev, 0)) != hipSuccess) return e;
-  }
-  if ((e = hipMemsetAsync(g.pmax_out, 0, (size_t)ngran * 8, st)) != hipSuccess) return e;
-  k_gemm_wsx<<<dim3(8 * 4 * ng), dim3(512), 0, st>>>(g);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (cap == hipStreamCaptureStatusNone) return hipEventRecord(ev, st);
-  return hipSuccess;
+  k_gemm_wsx<<<dim3(4 * 8 * ng), dim3(512), 0, st>>>(g);
+  return hipGetLastError();
 }
 
 hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {

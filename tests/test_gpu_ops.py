@@ -456,7 +456,7 @@ def test_linear_rows_ws(torch, oracle_model, monkeypatch, M, nopipe):
     # workgroups inside the launch; pmax_in unused, pmax_out = exchange scratch)
     h8b = torch.zeros_like(h8)
     shb = torch.full((M,), -1.0, dtype=torch.float32, device="cuda")
-    gx = torch.empty(((32 * M + 1024) // 4,), dtype=torch.float32, device="cuda")
+    gx = torch.empty(((32 * M + 2048) // 4,), dtype=torch.float32, device="cuda")
     _rows_call(torch, **{**base, "kp": 3}, epi=3, pmax_out=gx, out8=h8b, ldo8=2048, os=shb)
     np.testing.assert_array_equal(_from_kp(h8b.cpu().numpy(), M), qh)
     np.testing.assert_array_equal(shb.cpu().numpy(), s)
