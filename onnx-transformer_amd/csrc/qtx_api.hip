@@ -850,8 +850,8 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
 // streams, the second half one kernel behind, so the HBM-bound epilogues (residual +
 // LayerNorm) of one half overlap the MFMA / VALU-bound kernels (attention, FFN) of the
 // other on different CUs.  Results are identical (rows are independent).
-// (not with the one-pass FFN1: its workgroups wait for their partner slices, which two
-// concurrent launches on two streams could keep from ever being resident together)
+// (not with the one-pass FFN1, which makes the layer's kernels MFMA / exchange-bound rather
+// than HBM-bound: the split measured no gain before it, 2.07 vs 2.05 ms)
 bool wsx_on();
 bool enc_split(int B) { return B >= 256 && !getenv("QTX_ENC_NOSPLIT") && !wsx_on(); }
 

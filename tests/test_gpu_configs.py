@@ -90,9 +90,10 @@ def test_cfg3_encoder_sample_matches_oracle(torch, oracle_model, cfg3_inputs, cf
 
 def test_cfg3_encoder_split_two_threads(torch, gpu_model, cfg3_inputs, cfg3_split):
     """Two threads share the model handle, each on its own stream with its own inputs, at
-    the same time: the one-pass FFN1 launches of the two streams (whose workgroups wait for
-    their partner slices) are serialized per device, and with QTX_NO_WSX the two-stream split
-    path's shared second stream and fork / lag / join events by the model's lock."""
+    the same time: the two streams' one-pass FFN1 launches, whose workgroups wait for their
+    partner slices, run concurrently (work by arrival ticket: no co-residency requirement);
+    with QTX_NO_WSX the two-stream split path's shared second stream and fork / lag / join
+    events are serialized by the model's lock."""
     x, m = cfg3_inputs
     x2 = np.ascontiguousarray(x[::-1])      # a different batch: the sentences reversed
     m2 = np.ascontiguousarray(m[::-1])
