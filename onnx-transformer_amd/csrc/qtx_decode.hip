@@ -274,6 +274,81 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
 }
 
 // =====================================================================================
+// k_skinny8: the decode FFN2 (K = 2048, fp32 hidden quantized per token from its partial
+// maxima, residual epilogue) on 8 waves: two waves per row quantize one half of it each
+// (16 values per lane: half the dependent quantization chain of k_skinny's one row per
+// wave), K split 8 ways (4 weight fragments per lane), exact int32 reduction over the 8
+// waves.  Rows per workgroup 4, 16 columns.  Bit-identical to k_skinny.
+// =====================================================================================
+__global__ __launch_bounds__(512) void k_skinny8_ffn2(SkinnyArgs g) {
+  constexpr int K = 2048, RB = 4, KW = K / 8, NS = KW / 64, LDA = K + 16;
+  __shared__ __attribute__((aligned(16))) uint8_t As[16 * LDA];
+  __shared__ float sas[16];
+  __shared__ v4i red[7][64];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * RB;
+  // 1. the A operand's loads first: row r = wave / 2, half = wave & 1 (1024 values)
+  const int r = wave >> 1, half = wave & 1;
+  const int m = min(m0 + r, g.M - 1);
+  float4 t[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    t[c] = *reinterpret_cast<const float4*>(g.X + (long)m * g.ldx + 4 * (lane + 64 * (4 * half + c)));
+  float pm[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) pm[u] = g.pmax_in[(long)min(lane + 64 * u, g.pmax_n - 1) * g.M + m];
+  // 2. then this wave's weight fragments and (wave 0) the epilogue operands
+  const int n = min(n0 + fr, g.N - 1);
+  uint4 wf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + wave * KW + 64 * s + 16 * fg);
+  const int col = n0 + fr, cc = min(col, g.N - 1);
+  const bool cok = col < g.N;
+  const float swc = g.sw[cc], bc = g.bias[cc];
+  float rv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) rv[e] = g.res[(long)min(m0 + 4 * fg + e, g.M - 1) * g.ldr + cc];
+  // 3. per-token quantization of the half row into LDS
+  {
+    const bool ok = m0 + r < g.M;
+    const float sc = quant_scale(wave_max(fmaxf(pm[0], pm[1])), 127.0f);
+    float tf[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      tf[4 * c] = t[c].x; tf[4 * c + 1] = t[c].y; tf[4 * c + 2] = t[c].z; tf[4 * c + 3] = t[c].w;
+    }
+    uint32_t qd[4];
+    quant_pack<16>(tf, sc, qd);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(As + r * LDA);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dst[lane + 64 * (4 * half + c)] = ok ? qd[c] : 0u;
+    if (lane == 0 && half == 0) sas[r] = ok ? sc : 0.0f;
+  }
+  __syncthreads();
+  // 4. MFMA over this wave's K range, exact int32 reduction of the 8 ranges
+  v4i acc = v4i{0, 0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const v4i afr = *reinterpret_cast<const v4i*>(As + fr * LDA + wave * KW + 64 * s + 16 * fg);
+    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, __builtin_bit_cast(v4i, wf[s]), acc, 0, 0, 0);
+  }
+  if (wave > 0) red[wave - 1][lane] = acc;
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int w = 0; w < 7; ++w) acc += red[w][lane];
+  // 5. epilogue: out = res + y (rows 4fg + e < RB of the 16-row MFMA tile)
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int rr = 4 * fg + e, row = m0 + rr;
+    const float y = ((float)acc[e] * sas[rr]) * swc + bc;
+    if (cok && rr < RB && row < g.M) g.out[(long)row * g.ldo + col] = rv[e] + y;
+  }
+}
+
+// =====================================================================================
 // k_skinny_wide: the K = 512 skinny GEMM with N split over the 4 waves instead of K — a
 // workgroup covers 64 columns (wave w: columns n0 + 16w .. +15, all 8 K steps, 8 weight
 // fragments = 128 B per lane in flight) and its RB rows; no cross-wave reduction.  The
@@ -446,6 +521,12 @@ hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
     if (g.amode == A_LN) return skinny_rb<512, WB, A_LN>(g, rb_ln, st);
     if (g.amode == A_F32Q) return skinny_rb<512, WB, A_F32Q>(g, g.M <= 4 ? 4 : rb_i8, st);
   } else if (g.K == 2048) {
+    // the decode FFN2 (fp32 hidden, residual, 8-bit weights): 8 waves (QTX_SKINNY8=0: 4)
+    static const bool sk8 = env_rb("QTX_SKINNY8", 1) != 0;
+    if (sk8 && WB == 8 && g.amode == A_F32Q && g.flags == EPI_RESIDUAL && g.pmax_n <= 128) {
+      k_skinny8_ffn2<<<dim3(g.N / 16, (g.M + 3) / 4), 512, 0, st>>>(g);
+      return hipGetLastError();
+    }
     static const int rb_i8 = env_rb("QTX_RB_I8_2048", 4), rb_f = env_rb("QTX_RB_F32Q", 4);
     if (g.amode == A_I8) return skinny_rb<2048, WB, A_I8>(g, rb_i8, st);
     if (g.amode == A_F32Q) return skinny_rb<2048, WB, A_F32Q>(g, rb_f, st);
