@@ -53,7 +53,7 @@ def encoder_gemm_ops(B, S, n_layers=6):
     return n_layers * 2 * M * (3 * D * D + D * D + D * F + F * D)
 
 
-DOMINANT = "k_skinny<1,4,2048,8,A_F32Q,RESIDUAL>"   # FFN2 GEMM of the decode step (profiles/)
+DOMINANT = "k_skinny8_ffn2"   # FFN2 GEMM of the decode step (8-wave K=2048 skinny; profiles/)
 
 
 def dominant_alg_bytes(B):

@@ -13,7 +13,7 @@ import json
 import os
 import sys
 
-KERNEL = "k_skinny<1, 4, 2048, 8, 2, 2>"
+KERNEL = "k_skinny8_ffn2"
 
 
 def per_dispatch(d, counter):
