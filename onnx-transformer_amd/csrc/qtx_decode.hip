@@ -521,9 +521,11 @@ hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
     if (g.amode == A_LN) return skinny_rb<512, WB, A_LN>(g, rb_ln, st);
     if (g.amode == A_F32Q) return skinny_rb<512, WB, A_F32Q>(g, g.M <= 4 ? 4 : rb_i8, st);
   } else if (g.K == 2048) {
-    // the decode FFN2 (fp32 hidden, residual, 8-bit weights): 8 waves (QTX_SKINNY8=0: 4)
-    static const bool sk8 = env_rb("QTX_SKINNY8", 1) != 0;
-    if (sk8 && WB == 8 && g.amode == A_F32Q && g.flags == EPI_RESIDUAL && g.pmax_n <= 128) {
+    // the decode FFN2 (fp32 hidden, residual, 8-bit weights) at M <= QTX_SKINNY8_MAXM
+    // (default 32): 8 waves (measured: B = 32 decode 14.45 -> 14.40 ms; at B = 256 the
+    // 4-wave kernel is faster, 35.1 vs 36.8 ms)
+    static const int sk8_maxm = env_rb("QTX_SKINNY8_MAXM", 32);
+    if (g.M <= sk8_maxm && WB == 8 && g.amode == A_F32Q && g.flags == EPI_RESIDUAL && g.pmax_n <= 128) {
       k_skinny8_ffn2<<<dim3(g.N / 16, (g.M + 3) / 4), 512, 0, st>>>(g);
       return hipGetLastError();
     }
