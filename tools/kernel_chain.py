@@ -118,3 +118,32 @@ N_LAUNCH = 12
 t_layer = chain_us(layer_seq) * 1  # us per layer_seq call = per layer
 print(f"B={B} decoder layer as the step's 8-kernel sequence: {t_layer:.1f} us "
       f"(sum of the single-kernel chains {tot + 2.6:.1f} us incl. the Oc twin)", flush=True)
+
+# the step's tail: final LayerNorm + generator (k_generator_mfma, fp32 MFMA chain) and the
+# log_softmax argmax + next embedding (k_argmax_embed), on the model's own weights
+if os.environ.get("QTX_CHAIN_TAIL", "1") != "0":
+    from qtx.model import QtxModel
+    from qtx.weights import ModelConfig, synthetic_state_dict
+    N_LAUNCH = N_LAUNCH_SAVE
+    NLAYER = 1
+    m = QtxModel(synthetic_state_dict(1), ModelConfig())
+    V = 4444
+    logits = torch.empty((B, V), device="cuda")
+    ids = torch.zeros((B, 1300), dtype=torch.int64, device="cuda")
+    stepd = torch.zeros(4, dtype=torch.int32, device="cuda")
+    xn = torch.empty((B, 512), device="cuda")
+    gids = torch.empty(B, dtype=torch.int64, device="cuda")
+    gws = torch.empty(B * V, device="cuda")
+    h = m.handle
+    gen = lambda st, l: _lib.call("qtx_generator", h, P(x), B, P(logits), P(gids), P(gws), gws.numel() * 4, st)
+    arg = lambda st, l: _lib.call("qtx_decode_argmax_embed", h, P(logits), B, P(ids), 1300, P(stepd), P(xn), st)
+    print(f"B={B} {'generator + logsoftmax_argmax (2 kernels)':40s} {chain_us(gen):6.2f} us/launch", flush=True)
+    stepd.zero_()
+    print(f"B={B} {'argmax_embed (log_softmax argmax + embed)':40s} {chain_us(arg):6.2f} us/launch", flush=True)
+    # the generator alone (QTX_STAMPS builds export it: QTX_LIB_PATH=.../libqtx_stamps.so)
+    raw = C.CDLL(os.environ["QTX_LIB_PATH"]) if "stamps" in os.environ.get("QTX_LIB_PATH", "") else None
+    if raw is not None:
+        gwt = T((rng.standard_normal((4448, 512)) * 0.03).astype(np.float32))   # packed strips
+        gb = T(np.zeros(V, np.float32))
+        genm = lambda st, l: raw.qtx_debug_generator(P(x), B, P(lna), P(lnb), P(gwt), P(gb), V, P(logits), st)
+        print(f"B={B} {'generator alone (k_generator_mfma, LN)':40s} {chain_us(genm):6.2f} us/launch", flush=True)
