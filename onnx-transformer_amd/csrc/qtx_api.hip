@@ -956,9 +956,12 @@ struct GreedyWS {
 };
 
 // Sub-batch split of the fused decode.  Sentences are independent (per-token quantization:
-// no value depends on another sentence), and one sub-batch's step is a chain of ~75
-// latency-bound kernels that each occupy a fraction of the 256 CUs, so G sub-batches on
-// G streams overlap almost perfectly.  QTX_DECODE_GROUPS overrides the default.
+// no value depends on another sentence), and one sub-batch's step is a chain of ~50
+// latency-bound kernels that each occupy a fraction of the 256 CUs.  In one process the
+// G sub-batch graphs on G streams measured slower than one graph, not overlapped (B = 32:
+// 16.2 / 21.6 ms for G = 1 / 2; B = 128: 23.4 / 26.9; B = 256: 35.1 / 35.7).  Two processes
+// sharing the GPU do overlap, which points at the runtime, not the CUs.
+// Default G = 1; QTX_DECODE_GROUPS overrides it (experiments).
 struct Groups {
   int G, Bg;   // G groups of Bg rows (the last one may be shorter)
   int b0(int i) const { return i * Bg; }
