@@ -959,8 +959,8 @@ struct GreedyWS {
 // no value depends on another sentence), and one sub-batch's step is a chain of ~50
 // latency-bound kernels that each occupy a fraction of the 256 CUs.  In one process the
 // G sub-batch graphs on G streams measured slower than one graph, not overlapped (B = 32:
-// 16.2 / 21.6 ms for G = 1 / 2; B = 128: 23.4 / 26.9; B = 256: 35.1 / 35.7).  Two processes
-// sharing the GPU do overlap, which points at the runtime, not the CUs.
+// 16.2 / 21.6 ms for G = 1 / 2; B = 128: 23.4 / 26.9; B = 256: 35.1 / 35.7): the groups
+// overlap only partly, and one graph over the whole batch is at least as fast.
 // Default G = 1; QTX_DECODE_GROUPS overrides it (experiments).
 struct Groups {
   int G, Bg;   // G groups of Bg rows (the last one may be shorter)
