@@ -53,72 +53,134 @@ def encoder_gemm_ops(B, S, n_layers=6):
     return n_layers * 2 * M * (3 * D * D + D * D + D * F + F * D)
 
 
-DOMINANT = "k_skinny8_ffn2"   # FFN2 GEMM of the decode step (8-wave K=2048 skinny; profiles/)
+# The decode step's dominant kernel class (most time per cfg2 step in the rocprofv3 kernel
+# stats, profiles/r02q_bench_kernel_stats.md "by launch grid", B = 32 grids: 12 launches per
+# step x 4.60 us = 55 us, ahead of cross-attention 31 and FFN2 33): the attention output
+# projections O / Oc (attention.py:67 + sublayer_connection.py:17) — the fp32 context
+# quantized per token in the prologue from the 8 per-head partial maxima, residual epilogue.
+DOMINANT = "k_skinny<1, 4, 512, 8, 2, 2>"
+DOMINANT_COPIES = 32   # rotating operand sets: 8 MB of weights, more than an XCD's 4 MB L2
 
 
 def dominant_alg_bytes(B):
-    """Algorithmic bytes of one FFN2 decode launch (position_feed_forward.py:12 + the
-    residual, sublayer_connection.py:17): int8 W [512, 2048] + fp32 hidden [B, 2048] (quantized
-    per token in the prologue) + its partial row maxima [128, B] + per-channel scale/bias +
+    """Algorithmic bytes of one O-projection decode launch: int8 W [512, 512] + fp32 context
+    [B, 512] + its per-head partial row maxima [8, B] + per-channel scale and bias +
     fp32 residual in and out [B, 512]."""
-    N, K = D, F
-    return N * K + B * K * 4 + (F // 16) * B * 4 + 2 * N * 4 + 2 * B * N * 4
+    N, K = D, D
+    return N * K + B * K * 4 + 8 * B * 4 + 2 * N * 4 + 2 * B * N * 4
 
 
-def run_dominant(B, iters, stream=None):
-    """Launch the decode step's dominant kernel `iters` times (shapes of the real model:
-    M=B rows, N=512, K=2048, per-token quantization of the fp32 hidden from its partial
-    maxima in the prologue, residual epilogue).  Returns (launch fn, keepalive)."""
+def run_dominant(B, copies=DOMINANT_COPIES):
+    """The decode step's dominant kernel at M = B rows, N = K = 512, as the step launches it
+    (qtx_api.hip greedy_step_fused: amode A_F32Q with pmax_n = 8, EPI_RESIDUAL, out == res),
+    over `copies` rotating operand sets so weights come from MALL as in the step, not from an
+    L2-warm copy.  Returns (one(i): launch on operand set i % copies, on torch's current
+    stream; keepalive)."""
     import ctypes as C
 
     import torch
 
     from qtx import _lib
     rng = np.random.default_rng(1)
-    h = torch.from_numpy(np.maximum(rng.standard_normal((B, F)), 0).astype(np.float32)).cuda()
-    pm = h.abs().reshape(B, F // 16, 16).amax(-1).t().contiguous()   # [F/16][B]
-    w = torch.from_numpy(rng.integers(-127, 128, (D, F)).astype(np.int8)).cuda()
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    sets = []
+    for _ in range(copies):
+        ctx = rng.standard_normal((B, D)).astype(np.float32)
+        pm = np.abs(ctx).reshape(B, 8, 64).max(-1).T.copy()          # [8][B] per head
+        sets.append((T(ctx), T(pm), T(rng.integers(-127, 128, (D, D)).astype(np.int8)),
+                     T(rng.standard_normal((B, D)).astype(np.float32))))
     sw = torch.full((D,), 0.01, device="cuda")
     bias = torch.zeros(D, device="cuda")
-    res = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).cuda()
-    out = torch.empty((B, D), device="cuda")
-    st = C.c_void_p(stream if stream is not None else torch.cuda.current_stream().cuda_stream)
     P = lambda t: C.c_void_p(t.data_ptr())
     S0 = C.c_void_p(0)
-    args = (2, S0, S0, P(h), F, S0, S0, P(pm), F // 16, P(w), P(sw), P(bias), B, D, F, 8, 2,
-            P(res), P(out), S0, st)
+    L = _lib.lib(build=False)
+    fn = L.qtx_skinny_linear
 
-    def launch():
-        for _ in range(iters):
-            _lib.call("qtx_skinny_linear", *args)
-    return launch, (h, pm, w, sw, bias, res, out)
+    def one(i):
+        ctx, pm, w, x = sets[i % copies]
+        st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        rc = fn(2, S0, S0, P(ctx), D, S0, S0, P(pm), 8, P(w), P(sw), P(bias), B, D, D, 8, 2,
+                P(x), P(x), S0, st)
+        if rc:
+            raise RuntimeError(f"qtx_skinny_linear: {L.qtx_last_error().decode()}")
+    return one, (sets, sw, bias)
 
 
-def time_dominant(B, iters=200):
-    """Average launch duration (s) of the dominant decode kernel, HIP events on the stream
-    the kernel is launched on (torch's current stream)."""
+def nop():
+    import ctypes as C
+
     import torch
-    launch, keep = run_dominant(B, 20)
-    launch()
-    launch, keep = run_dominant(B, iters)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    launch()
-    e1.record()
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / 1e3 / iters
+
+    from qtx import _lib
+    _lib.call("qtx_debug_nop", C.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+
+def graph_time(body, reps=5):
+    """Microseconds of one replay of a hipGraph capturing body() (HIP events on the replay
+    stream), the fastest of `reps` replays."""
+    import torch
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        body()                                   # warm (and allocates nothing new)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            body()
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s):
+            e0.record()
+            g.replay()
+            e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) * 1e3
+        best = t if best is None else min(best, t)
+    return best
+
+
+def time_dominant(B, n=256):
+    """(us per launch of the dominant kernel in a hipGraph chain of n launches, us per node
+    of a chain of n empty kernels): HIP events on the replay stream."""
+    one, keep = run_dominant(B)
+    chain = graph_time(lambda: [one(i) for i in range(n)]) / n
+    floor = graph_time(lambda: [nop() for _ in range(n)]) / n
+    del keep
+    return chain, floor
+
+
+def step_alg_bytes(B, S, keys):
+    """Algorithmic HBM bytes of one KV-cached decoder step (qtx_api.hip greedy_step_fused,
+    50 kernels) with `keys` self-attention keys: every operand each kernel must read or
+    write once — weights + scales/biases, K/V caches, fp32 activations between kernels,
+    generator, logits, embedding row."""
+    V, H = 4444, 8
+    lin = lambda N, K: N * K + 8 * N                      # int8 W + fp32 sw, bias
+    x, x4 = B * D * 4, lambda n: B * n * 4                # fp32 [B, 512] / [B, n]
+    per_layer = (lin(3 * D, D) + x + 8 * D + x4(3 * D)                      # LN + QKV
+                 + x4(3 * D) + B * keys * (2 * D + 8) + B * (2 * D + 8) + x + H * B * 4  # self-attn
+                 + dominant_alg_bytes(B)                                   # O + residual
+                 + lin(D, D) + x + 8 * D + x                              # LN + Qc
+                 + x + B * S * (2 * D + 8) + B * S + x + H * B * 4        # cross-attn
+                 + dominant_alg_bytes(B)                                   # Oc + residual
+                 + lin(F, D) + x + 8 * D + x4(F) + (F // 16) * B * 4      # LN + FFN1
+                 + lin(D, F) + x4(F) + (F // 16) * B * 4 + 2 * x)         # FFN2 + residual
+    tail = (V * D * 4 + V * 4 + x + 8 * D + x4(V)                          # final LN + generator
+            + x4(V) + B * 8 + B * D * 4 + D * 4 + x)                      # argmax + embed
+    return 6 * per_layer + tail
 
 
 def pmc_traffic():
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
-    (tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction), or None."""
+    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 PMC
+    passes over it (tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
+    correction), or None when no profile names this kernel."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_dominant.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        return json.load(f).get("traffic_bytes_per_launch")
+    for fn in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_dominant.json")), reverse=True):
+        with open(fn) as f:
+            d = json.load(f)
+        if d.get("kernel") == DOMINANT:
+            return d.get("traffic_bytes_per_launch")
+    return None
 
 
 def _quantized_rows(rng, M, K, relu=False):
@@ -217,6 +279,16 @@ def time_decode(model, B, S, L, steps=3, seed=1000):
     return (time.perf_counter() - t0) / steps
 
 
+def workload_name(args, G, world):
+    """The BASELINE.json config a run measures (cfg2: 32 sentences per GPU; cfg4: the same
+    with int4 weights; cfg5: 2048 sentences over the ranks)."""
+    if args.weight_bits == 4:
+        return "cfg4" if G == 32 * world else "int4 custom"
+    if G == 2048:
+        return "cfg5"
+    return "cfg2" if G == 32 * world else "custom"
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -236,6 +308,10 @@ def cpu_baseline(sd, B=32, S=72, max_len=72, seed=7):
 
     from oracle.torch_port import TorchPortModel
     threads = torch.get_num_threads()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     tp = TorchPortModel(sd)
     src, _ = make_src(np.random.default_rng(seed), B, S)
     mask = torch.from_numpy((src != 2)[:, None, :])
@@ -255,7 +331,10 @@ def cpu_baseline(sd, B=32, S=72, max_len=72, seed=7):
     return {"value": B * (max_len - 1) / t2, "unit": "decoded tokens/s", "cores": int(threads),
             "kind": "port",
             "sample": f"oracle/torch_port.py (the reference's fp32 fake-quant arithmetic in "
-                      f"torch, KV-cached) on {threads} threads of '{cpu_model()}': cfg2 greedy "
+                      f"torch, KV-cached) on {threads} threads of '{cpu_model()}' (torch's "
+                      f"thread count = OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}, this "
+                      f"host's CPU share per GPU; os.cpu_count()={os.cpu_count()} is the whole "
+                      f"host, {affinity} CPUs in this process's affinity mask): cfg2 greedy "
                       f"decode B={B}, S={S}, {max_len - 1} steps in {t2:.1f}s",
             "cfg1_b1_decode_tokens_per_s": (max_len - 1) / t1,
             "cfg3_encoder_s": t3,
@@ -355,12 +434,29 @@ def main():
         verified = bool((allids >= 0).all() and np.array_equal(ref, allids[pick]))
 
     if rank == 0:
-        kt = time_dominant(min(B, 32))
-        alg = dominant_alg_bytes(min(B, 32))
-        roof = {"kernel": f"{DOMINANT}: FFN2 decode GEMM (M={min(B, 32)}, N={D}, K={F}, int8)",
+        Bd = min(B, 32)
+        chain_us, nop_us = time_dominant(Bd)
+        kt = (chain_us - nop_us) * 1e-6         # kernel duration: chain node minus the floor
+        alg = dominant_alg_bytes(Bd)
+        roof = {"kernel": f"{DOMINANT}: decode O / Oc projection (M={Bd}, N={D}, K={D}, int8, "
+                          "fp32 context quantized per token in the prologue, residual epilogue)",
                 "bound": "hbm", "achieved": alg / kt / 1e9, "peak": PEAK_HBM / 1e9,
                 "unit": "GB/s", "frac": alg / kt / PEAK_HBM, "traffic": pmc_traffic(),
-                "avg_us": kt * 1e6, "alg_bytes_per_launch": alg}
+                "avg_us": kt * 1e6, "chain_node_us": chain_us, "empty_node_us": nop_us,
+                "alg_bytes_per_launch": alg,
+                "method": f"hipGraph chain of 256 launches over {DOMINANT_COPIES} rotating operand "
+                          "sets, HIP events on the replay stream, minus a chain of 256 empty "
+                          "kernels (per-node floor)"}
+        # the whole decode step: (decode of max_len - 1 steps) - (decode of 1 step), per step
+        t_full = time_decode(model, Bd, S, L)
+        t_one = time_decode(model, Bd, S, 2)
+        step_us = (t_full - t_one) / (L - 2) * 1e6
+        sb = np.mean([step_alg_bytes(Bd, S, k) for k in range(2, L)])
+        step = {"B": Bd, "us": step_us, "alg_bytes": float(sb), "achieved": sb / step_us / 1e3,
+                "unit": "GB/s", "frac": sb / (step_us * 1e-6) / PEAK_HBM, "kernels": 50,
+                "empty_node_us": nop_us, "chain_floor_us": 50 * nop_us,
+                "note": "us = (decode of 71 steps - decode of 1 step) / 70; alg_bytes averaged "
+                        "over the 70 steps' self-attention key counts"}
         # the public API path (numpy in, numpy out, fresh buffers each call)
         pub = []
         for _ in range(3):
@@ -376,13 +472,14 @@ def main():
                "vs_baseline": None,
                "dtype": "int8" if args.weight_bits == 8 else "int4w-int8a",
                "data": "synthetic (seeded src ids, random-init weights of the reference architecture)",
-               "config": {"workload": f"cfg2: greedy decode, src<=64 padded to {S}, max_len={L}, "
-                                      f"{G} sentences length-sorted over {world} rank(s)",
+               "config": {"workload": f"{workload_name(args, G, world)}: greedy decode, src<=64 "
+                                      f"padded to {S}, max_len={L}, {G} sentences length-sorted "
+                                      f"over {world} rank(s)",
                           "global_batch": G, "per_gpu_batch": B, "seq_len": S,
                           "parallelism": f"sentence-shard x{world}"},
                "ids_verified_vs_single_batch_sample": verified,
                "public_api_ms_per_decode": min(pub) * 1e3,
-               "roofline": roof}
+               "roofline": roof, "step": step}
         if not args.no_cfg3:
             Bc, Sc = 256, 128
             xs = torch.randn((Bc, Sc, D), device="cuda")

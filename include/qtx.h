@@ -46,7 +46,11 @@ typedef enum {
   QTX_E_INVALID = 1,   /* bad argument / shape (the reference raises on shape mismatch) */
   QTX_E_HIP = 2,       /* a HIP runtime error, message in qtx_last_error() */
   QTX_E_WORKSPACE = 3, /* workspace too small: see qtx_*_workspace_size */
-  QTX_E_UNSUPPORTED = 4
+  QTX_E_UNSUPPORTED = 4,
+  QTX_E_DEVICE = 5     /* a kernel flagged an error it cannot repair in the model's device
+                        * status word (k_gemm_wsx: FFN1 row-max exchange timed out, outputs
+                        * invalid); reported by qtx_model_check, or by the next model-level
+                        * call on the model once the earlier call's work has finished */
 } qtx_status;
 
 typedef struct qtx_model qtx_model;
@@ -113,6 +117,11 @@ int32_t qtx_decoder_forward(const qtx_model* m, const float* y, const float* mem
 int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t* src_mask,
                           int32_t B, int32_t S, int32_t max_len, int64_t start, int64_t* ids,
                           void* ws, size_t ws_bytes, void* stream);
+
+/* Synchronise `stream`, then report (and clear) the model's device status word: QTX_OK, or
+ * QTX_E_DEVICE if a kernel of an earlier call on this model flagged an error (the outputs
+ * of that call are invalid).  The Python layer calls it wherever it synchronises anyway. */
+int32_t qtx_model_check(const qtx_model* m, void* stream);
 
 /* ---- fault injection (the reference's campaigns: inject_utils/layers.py:48-84,
  * onnx_optimized_inference.py:59-204, parallelized_inject_onnx_transformer.py:536-720) ----
@@ -254,6 +263,11 @@ typedef struct qtx_row_gemm {
    * pmax_in / pmax_n are not read; pmax_out is the exchange scratch (>= 32 * M + 2048 bytes,
    * overwritten).  The encoder's FFN1 (qtx_encoder_forward at M >= 2048). */
   int32_t kp;
+  /* kp = 3 only: device word OR-ed with 1 when a wait for the partner slices' row maxima
+   * timed out (the affected codes came from a partial maximum: the call's outputs are
+   * invalid).  NULL: the flag is the u32 at byte offset 1024 * ceil(M / 32) + 4 of pmax_out,
+   * zeroed by each launch; read it after the stream completes. */
+  uint32_t* status;
 } qtx_row_gemm;
 int32_t qtx_linear_rows(const qtx_row_gemm* args, void* stream);
 /* W int8 [N, K] row-major -> out [N, K] in the KP layout with the per-512-column-tile row
@@ -301,6 +315,11 @@ int32_t qtx_decode_attention(int32_t kv_new, const float* y, int64_t ldy, int8_t
 int32_t qtx_decode_argmax_embed(const qtx_model* m, const float* logits, int32_t M,
                                 int64_t* ids, int64_t ids_bs, int32_t* step_dev,
                                 float* x_next, void* stream);
+
+/* An empty one-wave kernel on `stream`: the dependent-launch floor that bench.py subtracts
+ * from a chain of launches to get per-kernel durations (measurement only, no reference
+ * counterpart). */
+int32_t qtx_debug_nop(void* stream);
 
 #ifdef __cplusplus
 }

@@ -114,6 +114,12 @@ struct qtx_model {
   hipStream_t estream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_lag = nullptr, ev_join = nullptr;
   int device = 0;            // the device the model's memory lives on
+  // device status word (DEV_E_* bits OR-ed by kernels that detect an error they cannot
+  // repair: k_gemm_wsx's exchange timeout) and its pinned host mirror, copied at the end
+  // of every model-level call and checked at the start of the next one (qtx_model_check:
+  // at once, after synchronising the caller's stream)
+  unsigned* status_dev = nullptr;
+  unsigned* status_host = nullptr;
   // an exec may still be running on a caller's stream: wait for its last replay first
   void clear_graphs() {
     for (auto& kv : graphs) {
@@ -143,6 +149,27 @@ struct DeviceGuard {
 }  // namespace
 
 namespace {
+
+// ---- the device status word ------------------------------------------------------------
+const char* status_text(unsigned v) {
+  return (v & DEV_E_EXCHANGE_TIMEOUT)
+             ? "k_gemm_wsx: the in-launch exchange of FFN1 row maxima timed out (the encoder's "
+               "FFN hidden was quantized from a partial row maximum): outputs invalid"
+             : "device status word set";
+}
+// at the start of a model-level call: an error an earlier call on this model left behind
+// (its mirror landed) is reported now, and cleared
+int status_pending(const qtx_model* m, hipStream_t st) {
+  const unsigned v = __atomic_exchange_n(m->status_host, 0u, __ATOMIC_ACQ_REL);
+  if (!v) return QTX_OK;
+  HIPCHK(hipMemsetAsync(m->status_dev, 0, sizeof(unsigned), st));
+  return fail(QTX_E_DEVICE, "%s (reported by a previous call on this model)", status_text(v));
+}
+// at the end of a model-level call: the mirror of the word follows the call's kernels
+int status_publish(const qtx_model* m, hipStream_t st) {
+  HIPCHK(hipMemcpyAsync(m->status_host, m->status_dev, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  return QTX_OK;
+}
 
 // ---- model layout ---------------------------------------------------------------------
 // Linear order per layer follows qtx/weights.py:linear_names():
@@ -245,6 +272,7 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     float* gb = ar.take<float>(c.tgt_vocab);
     int8_t* tmp = ar.take<int8_t>((size_t)F * D);
     m->gen_wt = ar.take<float>((size_t)((c.tgt_vocab + 15) / 16) * 16 * D);
+    m->status_dev = ar.take<unsigned>(64);
     return std::make_tuple(norms, src_lut, tgt_lut, pe_d, gw, gb, tmp);
   };
   qtx_model* m = new qtx_model();
@@ -329,6 +357,10 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
   m->src_lut = src_lut; m->tgt_lut = tgt_lut; m->pe = pe_d; m->gen_w = gw; m->gen_b = gb;
   he = launch_pack_gen(gw, c.tgt_vocab, m->gen_wt, st);
   if (he != hipSuccess) { qtx_model_destroy(m); return fail(QTX_E_HIP, "pack generator"); }
+  he = hipMemsetAsync(m->status_dev, 0, sizeof(unsigned), st);
+  if (he == hipSuccess) he = hipHostMalloc(reinterpret_cast<void**>(&m->status_host), sizeof(unsigned));
+  if (he != hipSuccess) { qtx_model_destroy(m); return fail(QTX_E_HIP, "status word"); }
+  *m->status_host = 0u;
   he = hipStreamSynchronize(st);
   if (he != hipSuccess) {
     qtx_model_destroy(m);
@@ -352,6 +384,7 @@ int32_t qtx_model_destroy(qtx_model* m) {
     if (m->gstream[i]) (void)hipStreamDestroy(m->gstream[i]);
   }
   if (m->mem) (void)hipFree(m->mem);
+  if (m->status_host) (void)hipHostFree(m->status_host);
   delete m;
   return QTX_OK;
 }
@@ -578,12 +611,13 @@ bool wsx_on() {
 }
 int row_ffn1(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa, int M,
              Scratch& s, hipStream_t st,
-             const FaultArgs& fa = FaultArgs{}, bool kp = false) {
+             const FaultArgs& fa = FaultArgs{}, bool kp = false, unsigned* status = nullptr) {
   RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RELU_PMAX, kp);
   if (g.kp == 2 && L.N == 2048 && fa.kind == FK_NONE && wsx_on()) {
     g.epi = RE_RELU_QUANT_PMAX;
     g.pmax_out = s.y;                // granules + ticket: <= 32 * M + 2048 bytes of the (unused) fp32 GEMM scratch
     g.out8 = s.h8; g.ldo8 = c.d_ff; g.os = s.sh;
+    g.status = status;               // the model's status word: a timeout becomes an error
     HIPCHK(launch_gemm_wsx(g, st));
     return QTX_OK;
   }
@@ -835,7 +869,7 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
       HIPCHK(ea);
     }
     RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st, fa(G_O), kp));
-    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1), kp));
+    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1), kp, m->status_dev));
     if (l + 1 < NL)
       RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc[l + 1].ln[0], s.a8, s.sa, nullptr, st,
                     fa(G_FFN2), kp));
@@ -1208,9 +1242,11 @@ int32_t qtx_encoder_forward_fault(const qtx_model* m, const float* x, const uint
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
   hipStream_t st = (hipStream_t)stream;
+  RC(status_pending(m, st));
   if (!enc_split(B) || (f && f->kind != QTX_FAULT_NONE)) {
     Scratch s = carve_scratch(ar, m->cfg, (long)B * S);
-    return encoder_run(m, x, src_mask, B, S, out, s, st, f);
+    RC(encoder_run(m, x, src_mask, B, S, out, s, st, f));
+    return status_publish(m, st);
   }
   // The model's second stream and its three events are shared by every caller: the lock
   // is held across the whole record / wait sequence, so two threads' fork, lag and join
@@ -1237,7 +1273,7 @@ int32_t qtx_encoder_forward_fault(const qtx_model* m, const float* x, const uint
                  s1, mm->estream, nullptr));
   HIPCHK(hipEventRecord(mm->ev_join, mm->estream));
   HIPCHK(hipStreamWaitEvent(st, mm->ev_join, 0));
-  return QTX_OK;
+  return status_publish(m, st);
 }
 
 int32_t qtx_encoder_forward(const qtx_model* m, const float* x, const uint8_t* src_mask,
@@ -1371,6 +1407,7 @@ int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
                                    "qtx_decoder_forward_fault on the step's prefix)");
   RC(check_fault(m, f, 0, B, S, 0));
   hipStream_t st = (hipStream_t)stream;
+  RC(status_pending(m, st));
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
   GreedyWS g = carve_greedy(ar, c, B, S, max_len);
@@ -1380,7 +1417,19 @@ int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
   RC(greedy_run(m, g, src, B, S, max_len, start, f, st));
   HIPCHK(hipMemcpyAsync(ids, g.ids, (size_t)B * max_len * sizeof(int64_t),
                         hipMemcpyDeviceToDevice, st));
-  return QTX_OK;
+  return status_publish(m, st);
+}
+
+int32_t qtx_model_check(const qtx_model* m, void* stream) {
+  if (!m) return fail(QTX_E_INVALID, "null model");
+  DeviceGuard dg(m->device);
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  unsigned v = 0;
+  HIPCHK(hipMemcpy(&v, m->status_dev, sizeof v, hipMemcpyDeviceToHost));
+  v |= __atomic_exchange_n(m->status_host, 0u, __ATOMIC_ACQ_REL);
+  if (!v) return QTX_OK;
+  HIPCHK(hipMemset(m->status_dev, 0, sizeof(unsigned)));
+  return fail(QTX_E_DEVICE, "%s", status_text(v));
 }
 
 int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t* src_mask,
@@ -1581,6 +1630,7 @@ int32_t qtx_linear_rows(const qtx_row_gemm* a, void* stream) {
   g.res = a->res; g.xout = a->xout; g.ln_a = a->ln_a; g.ln_b = a->ln_b;
   g.lnq = a->lnq; g.lns = a->lns; g.lnout = a->lnout;
   g.pmax_out = a->pmax_out; g.pmax_in = a->pmax_in; g.pmax_n = a->pmax_n; g.kp = a->kp;
+  g.status = reinterpret_cast<unsigned*>(a->status);
   const bool ok = (g.epi == RE_QUANT && g.out8 && g.os) ||
                   (g.epi == RE_RES_LN && g.res && g.xout && g.ln_a && g.ln_b &&
                    (g.lnq ? g.lns != nullptr : g.lnout != nullptr)) ||
@@ -1653,6 +1703,11 @@ int32_t qtx_decode_attention(int32_t kv_new, const float* y, int64_t ldy, int8_t
   a.step = step_dev; a.S = S; a.mask = mask; a.kv_new = kv_new;
   a.ctx = ctx; a.pmax = pmax; a.B = B;
   HIPCHK(launch_dec_attn(a, B, (hipStream_t)stream));
+  return QTX_OK;
+}
+
+int32_t qtx_debug_nop(void* stream) {
+  HIPCHK(launch_nop((hipStream_t)stream));
   return QTX_OK;
 }
 

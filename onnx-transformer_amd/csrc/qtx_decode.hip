@@ -881,6 +881,8 @@ hipError_t launch_transpose(const float* in, int R, int Cc, float* out, hipStrea
 // values above max - ARG_DELTA can tie it.  Fast path (block-uniform): exactly one such
 // value — it is the maximum and the token.  Otherwise the exponentials go through LDS
 // for the canonical lane-split denominator (wave 0) and the first argmax of logp decides.
+// A non-finite row (any NaN or +inf, or only -inf) is all-NaN under torch's log_softmax,
+// and torch.max of it is index 0: that row's token is 0 (oracle log_softmax_argmax).
 // Then the block writes the next decoder input (embedding + PE of the token).
 // =====================================================================================
 constexpr int ARG_T = 1024, ARG_NV = 8, ARG_MAXV = ARG_T * ARG_NV;
@@ -904,7 +906,7 @@ __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int 
                                                        int max_pos, float* xnext) {
   __shared__ float Ev[ARG_MAXV];
   __shared__ float redf[16], lse_s;
-  __shared__ int redi[16], redc[16];
+  __shared__ int redi[16], redc[16], redb[16];
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   QTX_STAMP(0);
   const int s = *step;
@@ -915,13 +917,20 @@ __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int 
 #pragma unroll
   for (int i = 0; i < ARG_NV; ++i) t[i] = x[min(tid + ARG_T * i, V - 1)];   // clamped
   QTX_STAMP(1);
-  // max: order-free; every wave reduces the 16 wave maxima itself (no second barrier)
+  // max: order-free; every wave reduces the 16 wave maxima itself (no second barrier);
+  // with it the non-finite test: bit 0 = a NaN or +inf, bit 1 = a value above -inf
   float lm = -3.0e38f;
+  bool nonfin = false, fin = false;
 #pragma unroll
   for (int i = 0; i < ARG_NV; ++i)
-    if (tid + ARG_T * i < V) lm = fmaxf(lm, t[i]);
+    if (tid + ARG_T * i < V) {
+      lm = fmaxf(lm, t[i]);
+      nonfin |= !(t[i] < __builtin_inff());
+      fin |= t[i] > -__builtin_inff();
+    }
   lm = wave_max(lm);
-  if (lane == 0) redf[w] = lm;
+  const int flags = (__ballot(nonfin) ? 1 : 0) | (__ballot(fin) ? 2 : 0);
+  if (lane == 0) { redf[w] = lm; redb[w] = flags; }
   __syncthreads();
   const float mx = wave_max(lane < 16 ? redf[lane] : -3.0e38f);
   // candidates for the first argmax of logp, and the first index of the maximum
@@ -940,8 +949,12 @@ __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int 
   __syncthreads();
   cnt = wave_sum_i32(lane < 16 ? redc[lane] : 0);
   int id = wave_min_i32(lane < 16 ? redi[lane] : 0x7fffffff);
+  const bool bad = __ballot(lane < 16 && (redb[lane] & 1)) != 0ull ||
+                   __ballot(lane < 16 && (redb[lane] & 2)) == 0ull;
   QTX_STAMP(2);
-  if (cnt != 1) {   // near-tie (or non-finite row): the exact log-softmax decides (block-uniform)
+  if (bad) {
+    id = 0;                                // torch.max of an all-NaN log_softmax row
+  } else if (cnt != 1) {   // near-tie: the exact log-softmax decides (block-uniform)
     // e_v = qexp(x_v - max) into LDS for the ordered sum
 #pragma unroll
     for (int i = 0; i < ARG_NV; ++i) {
@@ -979,7 +992,7 @@ __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int 
     const float gv = lane < 16 ? redf[lane] : -3.0e38f;
     const float gb = wave_max(gv);
     id = wave_min_i32(lane < 16 && gv == gb ? redi[lane] : 0x7fffffff);
-    id = min(id, V - 1);                   // all-NaN row guard: keep the embedding gather in bounds
+    id = min(id, V - 1);                   // keeps the embedding gather in bounds, whatever
   }
   if (tid == 0) ids[m * ids_bs + s + 1] = id;
   QTX_STAMP(4);

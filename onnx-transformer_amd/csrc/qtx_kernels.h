@@ -141,7 +141,15 @@ struct RowGemmArgs {
   // pack_w_kp), and the int8 lnq / RELU_QUANT out8 outputs written KP (RE_QUANT outputs
   // stay row-major: attention reads them); no fault support
   int kp;
+  // k_gemm_wsx (kp = 3): device status word OR-ed with DEV_E_EXCHANGE_TIMEOUT when a wait
+  // for the partner slices' row maxima hit its spin bound (that block's codes were then
+  // quantized from a partial maximum: the host must report the error, never use them);
+  // nullptr: the u32 after the ticket counter in the exchange scratch.  spin_limit: polls
+  // per wait before giving up (0: the launcher's default).
+  unsigned* status;
+  int spin_limit;
 };
+enum : unsigned { DEV_E_EXCHANGE_TIMEOUT = 1u };
 // W [N, K] int8 row-major -> KP layout with the row GEMM's column permutation per 512-wide
 // tile (LDS row rho holds column (rho & ~127) + 8 (rho & 15) + ((rho >> 4) & 7))
 hipError_t launch_pack_w_kp(const int8_t* W, int N, int K, int8_t* out, hipStream_t st);

@@ -454,7 +454,9 @@ hipError_t launch_generator(const float* x, long ldx, int M, const float* W, con
 
 // =====================================================================================
 // k_lsm_argmax: one wave per row.  z = x - max; lse = log(lane-split sum of qexp(z));
-// logp = z - lse; id = first index of the maximum logp (torch.max tie rule).
+// logp = z - lse; id = first index of the maximum logp (torch.max tie rule).  A row with a
+// NaN or a +inf, or only -inf, is all-NaN under torch's log_softmax and its torch.max is
+// index 0 (oracle log_softmax_argmax): logp NaN, id 0.
 // =====================================================================================
 __global__ __launch_bounds__(64) void k_lsm_argmax(const float* logits, int V, float* logp,
                                                    int64_t* ids, long ids_bs,
@@ -462,7 +464,18 @@ __global__ __launch_bounds__(64) void k_lsm_argmax(const float* logits, int V, f
   const int m = blockIdx.x, lane = threadIdx.x;
   const float* x = logits + (long)m * V;
   float lm = -3.0e38f;
-  for (int v = lane; v < V; v += 64) lm = fmaxf(lm, x[v]);
+  bool nonfin = false, fin = false;
+  for (int v = lane; v < V; v += 64) {
+    lm = fmaxf(lm, x[v]);
+    nonfin |= !(x[v] < __builtin_inff());
+    fin |= x[v] > -__builtin_inff();
+  }
+  if (__ballot(nonfin) != 0ull || __ballot(fin) == 0ull) {     // wave-uniform
+    if (logp)
+      for (int v = lane; v < V; v += 64) logp[(long)m * V + v] = __builtin_nanf("");
+    if (lane == 0 && ids) ids[m * ids_bs + (col_dev ? *col_dev : 0) + col_add] = 0;
+    return;
+  }
   const float mx = wave_max(lm);
   float ls = 0.0f;
   for (int v = lane; v < V; v += 64) ls = ls + qexp(x[v] - mx);

@@ -693,10 +693,12 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
 // an iteration earlier — the hand-off latency hides under a whole iteration.
 // Work is assigned by arrival ticket (below), so a row group only waits for partners that
 // have started or will start once other groups finish: no co-residency assumption, safe
-// beside any other launch.  Every spin is still bounded (a timed-out block would be
-// quantized with its own slice maximum: wrong, never hung — the parity tests catch it).
-// The granule array (4 x 32 x ceil(M/32) u64 + the ticket counter, in g.pmax_out) is
-// zeroed before every launch.
+// beside any other launch.  Every spin is still bounded (g.spin_limit polls): a wait that
+// times out sets DEV_E_EXCHANGE_TIMEOUT in *g.status, which the host turns into an error
+// (qtx_model_check / the next model call; qtx_linear_rows callers read the word) — a block
+// quantized from a partial maximum is never silent.
+// The granule array (4 x 32 x ceil(M/32) u64 + the ticket counter + the status word, in
+// g.pmax_out) is zeroed before every launch.
 // =====================================================================================
 __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
   constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
@@ -825,6 +827,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   // the row maximum over all 4 slices: this slice's, then the partners' granules (bounded)
+  const unsigned lim = (unsigned)g.spin_limit;
   auto full_max = [&](int k, float mloc) {
     const int rb = rbk(k);
     float m = mloc;
@@ -839,7 +842,12 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
         mx = fmaxf(mx, __uint_as_float((unsigned)v));
       }
       if (__all(ok)) { m = mx; break; }
-      if (spin > (1u << 18)) break;                 // bounded: never hang
+      if (spin >= lim) {                            // bounded: never hang, never silent
+        if (lane == 0)
+          __hip_atomic_fetch_or(g.status, DEV_E_EXCHANGE_TIMEOUT, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
       __builtin_amdgcn_s_sleep(2);
     }
     return m;
@@ -949,7 +957,17 @@ hipError_t launch_gemm_wsx(const RowGemmArgs& g, hipStream_t st) {
   const long ngran = 4L * 32 * nb + 2;
   hipError_t e = hipMemsetAsync(g.pmax_out, 0, (size_t)ngran * 8, st);
   if (e != hipSuccess) return e;
-  k_gemm_wsx<<<dim3(4 * 8 * ng), dim3(512), 0, st>>>(g);
+  RowGemmArgs a = g;
+  if (!a.status)                              // the u32 after the ticket counter
+    a.status = reinterpret_cast<unsigned*>(g.pmax_out) + 2 * (4L * 32 * nb) + 1;
+  if (a.spin_limit <= 0) {
+    // 2^18 polls x s_sleep 2 (~14 ms): far beyond any partner's start under load.  The
+    // environment override exists for the test that makes the timeout path fire.
+    const char* v = getenv("QTX_WSX_SPIN_LIMIT");
+    a.spin_limit = v && *v ? atoi(v) : (1 << 18);
+    if (a.spin_limit < 0) a.spin_limit = 0;
+  }
+  k_gemm_wsx<<<dim3(4 * 8 * ng), dim3(512), 0, st>>>(a);
   return hipGetLastError();
 }
 

@@ -39,7 +39,7 @@ class RowGemm(C.Structure):
                 ("out8", P), ("ldo8", I64), ("o8_ts", I64), ("os", P), ("os_ts", I64),
                 ("res", P), ("xout", P), ("ln_a", P), ("ln_b", P),
                 ("lnq", P), ("lns", P), ("lnout", P),
-                ("pmax_out", P), ("pmax_in", P), ("pmax_n", I32), ("kp", I32)]
+                ("pmax_out", P), ("pmax_in", P), ("pmax_n", I32), ("kp", I32), ("status", P)]
 
 class Fault(C.Structure):
     """struct qtx_fault (include/qtx.h)."""
@@ -85,6 +85,8 @@ SIGNATURES = {
                                 I32, P, P, P, P]),
     "qtx_decode_attention": (I32, [I32, P, I64, P, P, P, P, I32, P, I32, P, I32, P, P, P]),
     "qtx_decode_argmax_embed": (I32, [P, P, I32, P, I64, P, P, P]),
+    "qtx_debug_nop": (I32, [P]),
+    "qtx_model_check": (I32, [P, P]),
 }
 
 

@@ -23,6 +23,7 @@ def greedy_decode(model: QtxModel, src, src_mask, max_len: int, start_symbol: in
     srcd = src_t.to(model.device, torch.int64).contiguous()
     md = to_u8_mask(src_mask, model.device).reshape(B, S)
     ys = model.greedy(srcd, md, max_len=max_len, start=start_symbol)
+    model.check()
     if was_numpy:
         return ys.cpu().numpy()
     return ys.to(src_t.device)
@@ -45,8 +46,9 @@ def greedy_decode_fault(model: QtxModel, src, src_mask, max_len: int, start_symb
     enc_fault = fault if fault is not None and fault.module == 0 else None
     dec_fault = fault if fault is not None and fault.module == 1 else None
     if dec_fault is None:                       # KV-cached fused decode, faulty encoder
-        return model.greedy(srcd, md, max_len=max_len, start=start_symbol,
-                            fault=enc_fault).cpu().numpy()
+        ys = model.greedy(srcd, md, max_len=max_len, start=start_symbol, fault=enc_fault)
+        model.check()
+        return ys.cpu().numpy()
     memory = model.encode(model.embed(srcd, "src"), md)
     ys = torch.full((B, 1), int(start_symbol), dtype=torch.int64, device=dev)
     for i in range(max_len - 1):
@@ -56,6 +58,7 @@ def greedy_decode_fault(model: QtxModel, src, src_mask, max_len: int, start_symb
                            fault=dec_fault if i == target_inference_number - 1 else None)
         _, nxt = model.generator(out[:, -1].contiguous(), want_logp=False)
         ys = torch.cat([ys, nxt[:, None]], dim=1)
+    model.check()
     return ys.cpu().numpy()
 
 

@@ -86,6 +86,13 @@ class QtxModel:
                 pass
             self.handle = None
 
+    @_on_device
+    def check(self):
+        """Synchronise the current stream and raise QtxError (status QTX_E_DEVICE) if a
+        kernel of an earlier call flagged an error in the model's device status word
+        (qtx_model_check); called wherever the host synchronises anyway."""
+        _lib.call("qtx_model_check", self.handle, _stream(self.device))
+
     @property
     def device_bytes(self) -> int:
         return int(_lib.lib().qtx_model_device_bytes(self.handle))

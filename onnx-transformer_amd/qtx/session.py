@@ -136,7 +136,9 @@ class InferenceSession:
         return fn(self.model, feeds)
 
     def run(self, output_names, input_feed: dict):
-        out = self.run_torch(input_feed).cpu().numpy()
+        t = self.run_torch(input_feed)
+        self.model.check()
+        out = t.cpu().numpy()
         if output_names not in (None, [], ["global_out"]):
             raise ValueError(f"unknown outputs {output_names}; the graph has ['global_out']")
         return [out]
@@ -177,6 +179,14 @@ def run_module(module, input_values, module_filepath=None, module_weight_dict=No
         targetted = str(inject_parameters.get("targetted_module", module))
         if "RANDOM" not in kind_ and str(module) not in targetted:
             inject_parameters = None
+        elif "RANDOM" in kind_:
+            # a name that is no MatMul of this module's graph matches no node there: the
+            # reference then injects nothing (onnx_optimized_inference.py:59)
+            try:
+                F.matmul_target(inject_parameters["faulty_operation_name"], kind,
+                                model.cfg.n_layers)
+            except ValueError:
+                inject_parameters = None
     if inject_parameters:
         if isinstance(inject_parameters, F.Fault):
             flt = inject_parameters
@@ -203,6 +213,8 @@ def run_module(module, input_values, module_filepath=None, module_weight_dict=No
         weight_dict.update(trace)
         weight_dict["global_out"] = out
         return {"global_out": out}, weight_dict
-    out = fn(model, input_values, flt).cpu().numpy()
+    t = fn(model, input_values, flt)
+    model.check()
+    out = t.cpu().numpy()
     weight_dict["global_out"] = out
     return {"global_out": out}, weight_dict

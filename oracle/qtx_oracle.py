@@ -101,6 +101,27 @@ def _butterfly(v):
     return v[..., 0]
 
 
+def log_softmax_argmax(logits):
+    """log_softmax over the last axis (generator.py:15) and torch.max's first index of the
+    maximum (reference/onnx_reference_inference.py:640-641), in the canonical order:
+    z = x - max, lse = log(lane-split sum of qexp(z)), logp = z - lse.
+    Non-finite rows follow torch: a row holding a NaN or a +inf, or only -inf, has an
+    all-NaN log_softmax (inf - inf, or a NaN that propagates), and torch.max of an all-NaN
+    row is index 0 (pinned against torch in tests/test_oracle_golden.py).
+    Returns (logp f32, ids int64)."""
+    x = np.asarray(logits, f32)
+    bad = np.isnan(x).any(-1) | np.isposinf(x).any(-1) | np.isneginf(x).all(-1)
+    xs = np.where(bad[:, None], f32(0), x)
+    m = xs.max(axis=-1)
+    z = (xs - m[:, None]).astype(f32)
+    lse = np.log(row_sum_lanesplit(qexp(z))).astype(f32)
+    lp = (z - lse[:, None]).astype(f32)
+    lp[bad] = np.nan
+    ids = lp.argmax(axis=-1)
+    ids[bad] = 0
+    return lp, ids
+
+
 def row_sum_lanesplit(x):
     """Sum over the last axis in the 'strided' canonical order.
 
@@ -510,12 +531,7 @@ class OracleModel:
     def generator(self, x):
         """Generator.forward (generator.py:14-15) + first-index argmax
         (reference/onnx_reference_inference.py:640-641).  Returns (logprobs, ids)."""
-        logits = self.logits(x)
-        m = logits.max(axis=-1)
-        z = logits - m[:, None]
-        lse = np.log(row_sum_lanesplit(qexp(z))).astype(f32)
-        lp = z - lse[:, None]
-        return lp.astype(f32), lp.argmax(axis=-1)
+        return log_softmax_argmax(self.logits(x))
 
     def greedy_decode(self, src, src_mask, max_len=72, start=0, kv_cache=True, fault=None,
                       fault_step=0):

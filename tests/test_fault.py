@@ -238,6 +238,23 @@ def test_run_module_fault_for_other_module_is_golden(torch_gpu, gpu_model, oracl
     np.testing.assert_array_equal(outs["global_out"], ref)
 
 
+@pytest.mark.gpu
+def test_run_module_random_fault_on_foreign_name_is_golden(torch_gpu, gpu_model, oracle_model,
+                                                           golden_model):
+    """A RANDOM fault names a node alone (onnx_optimized_inference.py:59): on a module whose
+    graph has no MatMul of that name (MatMul_60 is a decoder MatMul; the encoder's end at
+    MatMul_47) the reference finds nothing to inject and the run is golden."""
+    from qtx.session import run_module
+    feeds = {"global_in": golden_model["enc_in"], "global_in_1": golden_model["src_mask"]}
+    p = {"inject_type": "RANDOM", "faulty_operation_name": "MatMul_60",
+         "targetted_module": "Decoder", "faulty_bit_position": 3}
+    outs, wd = run_module("Encoder", feeds, None, {}, None, inject_parameters=p,
+                          model=gpu_model, rng=np.random.default_rng(3))
+    assert "qtx_fault" not in wd
+    ref = oracle_model.encode(golden_model["enc_in"], golden_model["src_mask"])
+    np.testing.assert_array_equal(outs["global_out"], ref)
+
+
 ATTN_CASES = [("INPUT", "QK"), ("INPUT16", "QK"), ("WEIGHT", "QK"), ("WEIGHT16", "QK"),
               ("RANDOM", "QK"), ("INPUT", "PV"), ("INPUT16", "PV"), ("WEIGHT", "PV"),
               ("WEIGHT16", "PV"), ("RANDOM", "PV")]

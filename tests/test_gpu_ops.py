@@ -210,6 +210,21 @@ def test_generator(torch, gpu_model, golden_ops, oracle_model):
     assert np.abs(logp.cpu().numpy() - lo).max() <= 2e-6
 
 
+def test_generator_nonfinite_rows(torch, gpu_model, golden_ops, oracle_model):
+    """qtx_generator on rows whose logits are non-finite (a NaN input; inputs so large the
+    logits overflow to +-inf): torch's rule, logp all NaN and id 0, as the oracle says."""
+    x = np.concatenate([golden_ops["gen_x"]] * 4)[:6].astype(f32)
+    x[0, 3] = np.nan
+    x[1] *= f32(1e37)
+    x[2, :] = f32(3e38)
+    logp, ids, logits = gpu_model.generator(dev(torch, x), return_logits=True)
+    lo, io = oracle_model.generator(x)
+    np.testing.assert_array_equal(ids.cpu().numpy(), io)
+    np.testing.assert_array_equal(np.isnan(logp.cpu().numpy()), np.isnan(lo))
+    assert io[0] == 0 and np.isnan(lo[0]).all()
+    assert not np.isfinite(logits.cpu().numpy()[1:3]).all()    # the overflow rows do overflow
+
+
 def _rows_call(torch, **kw):
     from qtx._lib import RowGemm, lib
     import ctypes as C

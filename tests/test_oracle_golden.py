@@ -91,6 +91,21 @@ def test_generator(golden_ops, oracle_model):
     np.testing.assert_array_equal(ids, golden_ops["gen_ref"].argmax(-1))
 
 
+def test_argmax_nonfinite_rows_follow_torch():
+    """The token rule on non-finite logits is the reference's own: torch.max over
+    F.log_softmax (generator.py:15, reference/onnx_reference_inference.py:640-641) — any
+    NaN, any +inf or an all -inf row gives an all-NaN row and index 0; a -inf among finite
+    values is just a zero probability.  torch here is the reference's CPU arithmetic."""
+    import torch
+    inf, nan = np.inf, np.nan
+    rows = np.array([[1, nan, 2, 0], [1, inf, 2, 0], [-inf] * 4, [1, -inf, 2, 0],
+                     [nan] * 4, [3, 1, 0, nan], [2, 5, 5, -1], [-inf, inf, 1, 1]], f32)
+    lp, ids = O.log_softmax_argmax(rows)
+    tl = torch.log_softmax(torch.from_numpy(rows), -1)
+    np.testing.assert_array_equal(ids, torch.max(tl, 1)[1].numpy())
+    np.testing.assert_array_equal(np.isnan(lp), np.isnan(tl.numpy()))
+
+
 def test_qexp_accuracy():
     x = np.linspace(-79.9, 3.0, 100001).astype(f32)
     e = O.qexp(x)

@@ -13,7 +13,8 @@ import json
 import os
 import sys
 
-KERNEL = "k_skinny8_ffn2"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import DOMINANT as KERNEL  # noqa: E402
 
 
 def per_dispatch(d, counter):
