@@ -436,17 +436,22 @@ def main():
     if rank == 0:
         Bd = min(B, 32)
         chain_us, nop_us = time_dominant(Bd)
-        kt = (chain_us - nop_us) * 1e-6         # kernel duration: chain node minus the floor
+        # per-launch time = one node of a dependent hipGraph chain, as the decode step runs
+        # it (its launch boundary included: conservative).  rocprofv3's per-dispatch
+        # durations of graph-replayed nodes are inflated by the profiler (an empty kernel
+        # reads 4.6 us there, 1.6 us per node live: profiles/r03b_dominant_timing.md)
+        kt = chain_us * 1e-6
         alg = dominant_alg_bytes(Bd)
         roof = {"kernel": f"{DOMINANT}: decode O / Oc projection (M={Bd}, N={D}, K={D}, int8, "
                           "fp32 context quantized per token in the prologue, residual epilogue)",
                 "bound": "hbm", "achieved": alg / kt / 1e9, "peak": PEAK_HBM / 1e9,
                 "unit": "GB/s", "frac": alg / kt / PEAK_HBM, "traffic": pmc_traffic(),
-                "avg_us": kt * 1e6, "chain_node_us": chain_us, "empty_node_us": nop_us,
-                "alg_bytes_per_launch": alg,
-                "method": f"hipGraph chain of 256 launches over {DOMINANT_COPIES} rotating operand "
-                          "sets, HIP events on the replay stream, minus a chain of 256 empty "
-                          "kernels (per-node floor)"}
+                "avg_us": kt * 1e6, "empty_node_us": nop_us,
+                "marginal_us": chain_us - nop_us, "alg_bytes_per_launch": alg,
+                "method": f"hipGraph chain of 256 dependent launches over {DOMINANT_COPIES} "
+                          "rotating operand sets, HIP events on the replay stream: us per node "
+                          "(launch boundary included); empty_node_us = the same chain of empty "
+                          "kernels, marginal_us = the difference"}
         # the whole decode step: (decode of max_len - 1 steps) - (decode of 1 step), per step
         t_full = time_decode(model, Bd, S, L)
         t_one = time_decode(model, Bd, S, 2)

@@ -221,6 +221,17 @@ int32_t qtx_attention_i8(const int8_t* q, const float* sq, const int8_t* k, cons
                          int64_t m_is, int32_t B, int32_t H, int32_t Sq, int32_t Sk,
                          float* ctx, void* stream);
 
+/* qtx_attention_i8 plus the attention MatMuls' intermediates, for the traced executor
+ * (run_module(expose_intermediates=...), onnx_optimized_inference.py:57 stores every node
+ * output by name): qk_acc [B,H,Sq,Sk] = float(sum_d q k), the exact integer accumulators of
+ * QK^T ("FirstMatMul" MatMul_{8L+3}, before the / 8 and the mask); p_codes [B,H,Sq,Sk] =
+ * rint(P * 127) (the Round of attention.py:33-35); ctx as qtx_attention_i8, bit for bit.
+ * qk_acc / p_codes may be NULL.  Off the hot path (one wave per query row and head). */
+int32_t qtx_attention_trace(const int8_t* q, const float* sq, const int8_t* k, const float* sk,
+                            const int8_t* v, const float* sv, const uint8_t* mask, int64_t m_bs,
+                            int64_t m_is, int32_t B, int32_t H, int32_t Sq, int32_t Sk,
+                            float* ctx, float* qk_acc, float* p_codes, void* stream);
+
 /* Encoder self-attention with the context quantized per token for the O-projection
  * (attention.py:23-67 + quant_linear.py:30-43, replacing the MatMul_{8L+3,8L+4} pair of the
  * encoder graph and the following QuantizeLinear): q/k/v int8 [B,S,512] (8 heads) +

@@ -1732,6 +1732,25 @@ int32_t qtx_pack_int4(const int8_t* q, int32_t N, int32_t K, uint8_t* packed, vo
   return QTX_OK;
 }
 
+int32_t qtx_attention_trace(const int8_t* q, const float* sq, const int8_t* k, const float* sk,
+                            const int8_t* v, const float* sv, const uint8_t* mask, int64_t m_bs,
+                            int64_t m_is, int32_t B, int32_t H, int32_t Sq, int32_t Sk,
+                            float* ctx, float* qk_acc, float* p_codes, void* stream) {
+  if (!q || !sq || !k || !sk || !v || !sv || !ctx) return fail(QTX_E_INVALID, "null argument");
+  if (Sk <= 0 || Sk > 512 || Sq <= 0 || B <= 0 || H <= 0)
+    return fail(QTX_E_UNSUPPORTED, "Sk=%d (max 512) Sq=%d B=%d H=%d", Sk, Sq, B, H);
+  const long D = (long)H * 64;
+  AttnArgs a{};
+  a.q = q; a.q_bs = Sq * D; a.q_ld = D; a.sq = sq; a.sq_bs = Sq;
+  a.k = k; a.k_bs = Sk * D; a.k_ld = D; a.sk = sk; a.sk_bs = Sk;
+  a.v = v; a.v_bs = Sk * D; a.v_ld = D; a.sv = sv; a.sv_bs = Sk;
+  a.mask = mask; a.m_bs = m_bs; a.m_is = m_is;
+  a.ctx = ctx; a.c_bs = Sq * D; a.c_ld = D;
+  a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
+  HIPCHK(launch_attn_trace(a, qk_acc, p_codes, (hipStream_t)stream));
+  return QTX_OK;
+}
+
 int32_t qtx_attention_i8_quant(const int8_t* q, const float* sq, const int8_t* k,
                                const float* sk, const int8_t* v, const float* sv,
                                const uint8_t* key_mask, int32_t B, int32_t S, int8_t* ctx8,

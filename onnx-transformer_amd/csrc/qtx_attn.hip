@@ -655,6 +655,75 @@ __global__ __launch_bounds__(64) void k_attn_fault_rows(AttnArgs a, AttnFault f)
   a.ctx[b * a.c_bs + (long)i * a.c_ld + hoff + d] = acc;
 }
 
+// =====================================================================================
+// k_attn_trace: the attention MatMuls' intermediates for the traced executor (qtx/trace.py:
+// the reference's node-by-node executor stores every node output by name,
+// onnx_optimized_inference.py:57).  One wave per (query row i, sentence b x head h), the
+// canonical order of the oracle (attention_scores / softmax_quant / attention_pv):
+//   qk [B,H,Sq,Sk]  float(sum_d q[i][d] k[j][d])  (QK^T "FirstMatMul", exact integers)
+//   pc [B,H,Sq,Sk]  rint(P * 127)                 (the Round of attention.py:33-35)
+//   ctx             sum_j (P/127) v_j s_v[j] per head, as launch_attention writes it
+// Off the hot path (diagnostics / campaigns): scalar int8 loads, one row per wave.
+// =====================================================================================
+__global__ __launch_bounds__(64) void k_attn_trace(AttnArgs a, float* qk, float* pc) {
+  __shared__ float Ps[512];
+  const int lane = threadIdx.x;
+  const int i = blockIdx.x, b = blockIdx.y / a.H, h = blockIdx.y % a.H, Sk = a.Sk;
+  const int hoff = 64 * h;
+  const long orow = ((long)blockIdx.y * a.Sq + i) * Sk;
+  const int8_t* qrow = a.q + b * a.q_bs + (long)i * a.q_ld + hoff;
+  const float sqi = a.sq[b * a.sq_bs + i];
+  float x[8];
+  float m = -3.0e38f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int j = lane + 64 * t;
+    x[t] = -3.0e38f;
+    if (j < Sk) {
+      const int8_t* krow = a.k + b * a.k_bs + (long)j * a.k_ld + hoff;
+      int acc = 0;
+      for (int d = 0; d < 64; ++d) acc += (int)qrow[d] * (int)krow[d];
+      if (qk) qk[orow + j] = (float)acc;
+      const float sc = (((float)acc * sqi) * a.sk[b * a.sk_bs + j]) / 8.0f;
+      const bool keep = !a.mask || a.mask[b * a.m_bs + (long)i * a.m_is + j] != 0;
+      x[t] = keep ? sc : -1.0e9f;
+      m = fmaxf(m, x[t]);
+    }
+  }
+  m = wave_max(m);
+  float part = 0.0f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int j = lane + 64 * t;
+    x[t] = j < Sk ? qexp(x[t] - m) : 0.0f;
+    if (64 * t < Sk) part = part + x[t];
+  }
+  const float den = wave_sum(part);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int j = lane + 64 * t;
+    if (j < Sk) {
+      const float n = rintf((x[t] / den) * 127.0f);
+      Ps[j] = n / 127.0f;
+      if (pc) pc[orow + j] = n;
+    }
+  }
+  __syncthreads();
+  const int d = lane;
+  float acc = 0.0f;
+  for (int j = 0; j < Sk; ++j) {
+    const float vb = (float)a.v[b * a.v_bs + (long)j * a.v_ld + hoff + d] * a.sv[b * a.sv_bs + j];
+    acc = fmaf(Ps[j], vb, acc);
+  }
+  a.ctx[b * a.c_bs + (long)i * a.c_ld + hoff + d] = acc;
+}
+
+hipError_t launch_attn_trace(const AttnArgs& a, float* qk, float* pc, hipStream_t st) {
+  if (a.Sk <= 0 || a.Sk > 512 || a.Sq <= 0 || a.B <= 0 || a.H <= 0) return hipErrorInvalidValue;
+  k_attn_trace<<<dim3(a.Sq, a.B * a.H), dim3(64), 0, st>>>(a, qk, pc);
+  return hipGetLastError();
+}
+
 hipError_t launch_attn_fault_rows(const AttnArgs& a, const AttnFault& f, hipStream_t st) {
   if (a.Sk <= 0 || a.Sk > 512 || f.nrows <= 0 || f.b < 0 || f.b >= a.B || f.h < 0 ||
       f.h >= a.H || f.row0 < 0 || f.row0 + f.nrows > a.Sq)

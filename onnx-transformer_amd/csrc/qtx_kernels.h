@@ -104,6 +104,10 @@ struct AttnFault {
   float value;
 };
 hipError_t launch_attn_fault_rows(const AttnArgs& a, const AttnFault& f, hipStream_t st);
+// The attention MatMuls' intermediates (k_attn_trace, canonical order): QK^T accumulators
+// qk [B,H,Sq,Sk] (float of the exact int), P codes pc [B,H,Sq,Sk] (rint(P*127)), and ctx as
+// launch_attention; qk / pc may be null.  Sk <= 512.
+hipError_t launch_attn_trace(const AttnArgs& a, float* qk, float* pc, hipStream_t st);
 
 // Row-complete int8 GEMM (large M, 8-bit weights, N % 512 == 0, K % 64 == 0): each
 // workgroup owns 128 rows x one 512-wide column tile, so epilogues that need a whole

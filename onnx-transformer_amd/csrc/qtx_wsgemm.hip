@@ -416,6 +416,19 @@ __global__ __launch_bounds__(512) void k_gemm_ws(RowGemmArgs g) {
 // waits with a counted vmcnt.
 // =====================================================================================
 constexpr int WP_R = 32, WP_STAGE = WP_R * WS_K;    // 16 KB A stage
+
+// Scheduling pattern for the compiler's IGroupLP: NM times {one MFMA, NV VALU} over the
+// current scheduling region, so the epilogue arithmetic of the previous block is spread
+// between this block's MFMAs instead of running before or after them (the matrix pipe
+// and the vector issue then overlap: tools/probe_mfma_valu.hip)
+template <int NM, int NV>
+__device__ __forceinline__ void interleave() {
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+  }
+}
 // s_waitcnt immediates (gfx9 encoding: vmcnt bits 3:0 and 15:14, expcnt 6:4, lgkmcnt 11:8)
 constexpr int WAIT_VM(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70 | 0xF00; }
 constexpr int WAIT_LGKM0 = 0xC07F;
@@ -567,7 +580,10 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
       // rint(y / s) exactly: div_cr (shared reciprocal per row) on y and s both scaled by
       // 2^-64 when the row max is >= 2^37 (an exact power-of-two scaling that keeps every
       // intermediate of the Markstein step normal; |y / s| <= 127 either way) — branch-free
-      const float sc = quant_scale(m, 127.0f);
+      // the scale by the true division (one per row and lane: cheap), not quant_scale's
+      // guarded shared-reciprocal form, whose wave-uniform branch would split this basic
+      // block and keep the quantization from interleaving with the MFMAs above
+      const float sc = fmaxf(m, 1e-5f) / 127.0f;
       const float kk = m < 0x1p37f ? 1.0f : 0x1p-64f;
       const float scs = sc * kk, invs = 1.0f / scs;
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc), srsrc, 4 * (m0 + (lane & 31)), 0, 0);
@@ -642,6 +658,9 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
     float y[2][16];
     mfma_steps(acc, cur, 0, 4);
     epi1(accp, sap, y);
+#ifdef QTX_WSP_IGLP
+    interleave<32, QTX_WSP_IGLP_V1>();
+#endif
     const long long t2 = QTX_NOW();
     st_h1 += t2 - t1;
     __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
@@ -650,6 +669,9 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
     st_mid += t3 - t2;
     mfma_steps(acc, cur, 4, 8);
     epi2(k - 1, y, pmp);
+#ifdef QTX_WSP_IGLP
+    interleave<32, QTX_WSP_IGLP_V2>();
+#endif
     st_h2 += QTX_NOW() - t3;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -677,6 +699,522 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
   QTX_STAMP_VAL(4, st_h2);
   QTX_STAMP_VAL(5, QTX_NOW() - st_0);
   QTX_STAMP_VAL(6, nblk);
+}
+
+// =====================================================================================
+// k_gemm_wsq: the weight-stationary Q/K/V GEMM (RE_QUANT) with ONE barrier per 32-row block
+// and the quantization one block behind, interleaved between the MFMAs in a fixed order:
+//   iteration k:  the 64 MFMAs of block k with one quantized output of block k-1 after every
+//                 second one (its row maxima in red[(k-1) & 1] are complete: every wave
+//                 wrote them at the end of iteration k-1, before this barrier); then, as a
+//                 VALU-only phase, y = ((acc * sa) * sw) + b of block k and its partial row
+//                 maxima -> red[k & 1].
+// Why this split (tools/probe_mfma_valu.hip, two waves per SIMD): about two VALU per i8
+// MFMA issue for free beside the matrix work, each further one costs ~4 cycles there,
+// while VALU with no MFMA to share the SIMD with costs ~2 cycles (the two waves
+// alternate).  The quantization (~4.5 VALU per output) fills exactly the free slots; y
+// (~5 per output) runs on its own.  The compiler's list scheduler puts MFMAs back to back
+// and the epilogue before or after them (k_gemm_wsp), so each MFMA here is an asm statement
+// (asm statements keep their order) and each quantized output is pinned between two of them
+// by operands the asm text does not touch: the previous output's result is an input of the
+// next MFMA, the next output's input an output of it.
+// Numerics as k_gemm_wsp: div_cr with the row's reciprocal (Markstein: RN(y / s) for every
+// y with |y| <= the row maximum, any magnitude), the scale by true division.
+// =====================================================================================
+// Z: the block's first K step, accumulator from the inline constant 0.  (Zeroing it with
+// VALU instead needs wait states before the MFMA reads it, which the compiler inserts only
+// for MFMAs it knows about, not for these asm statements.)
+template <bool Z, typename T>
+__device__ __forceinline__ void mfma_pin(v4i& acc, const v4i& w, const v4i& a, float before, T& after) {
+  // operands: %0 acc, %1 after (outputs first), %2 w, %3 a, %4 before
+  if constexpr (Z)
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %2, %3, 0" : "=&v"(acc), "+v"(after) : "v"(w), "v"(a), "v"(before));
+  else
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %2, %3, %0" : "+v"(acc), "+v"(after) : "v"(w), "v"(a), "v"(before));
+}
+template <bool Z>
+__device__ __forceinline__ void mfma_asm(v4i& acc, const v4i& w, const v4i& a) {
+  if constexpr (Z)
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, 0" : "=&v"(acc) : "v"(w), "v"(a));
+  else
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(acc) : "v"(w), "v"(a));
+}
+
+// After the last asm MFMA of a block: the compiler tracks no wait states for asm MFMAs, so
+// pad their results before anything reads them (every acc is an operand here, so no read,
+// copy or spill of one moves above the pad).
+__device__ __forceinline__ void mfma_settle(v4i (&acc)[2][4]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4"
+               : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[0][2]), "+v"(acc[0][3]),
+                 "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[1][2]), "+v"(acc[1][3]));
+}
+
+__global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
+  constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
+  // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias (4 KB) | red [2][8][32] (2 KB)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4];
+  uint8_t* const wl = lds + 2 * WP_STAGE;
+  float* const swl = reinterpret_cast<float*>(wl + WL);
+  float* const red0 = swl + 1024;                            // [2][8][32]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int f = lane & 15, gq = lane >> 4;
+  const int nsl = g.N >> 9;
+  const int wpt = gridDim.x / nsl;
+  const int t = blockIdx.x % nsl, r0 = blockIdx.x / nsl;
+  const int nb = (g.M + WP_R - 1) / WP_R;
+  if (r0 >= nb) return;
+  const int nblk = (nb - r0 + wpt - 1) / wpt;
+
+  auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto rbk = [&](int k) { return r0 + min(k, nblk - 1) * wpt; };
+  auto issue = [&](int k) {
+    uint8_t* st = lds + (k & 1) * WP_STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long row = min(rbk(k) * WP_R + 16 * i + f, g.M - 1);
+      dma16(g.A + kp_off(row, 64 * wave + 16 * gq, WS_K), st + ((wave * 2 + i) << 10));
+    }
+  };
+  issue(0);
+  v4i wr[SR][4];
+  {
+    const int8_t* wsrc = g.W + ((long)(t * 8 + wave) << 15);
+    const v4i* ws = reinterpret_cast<const v4i*>(wsrc) + lane;
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wr[s][j] = ws[(s * 4 + j) * 64];
+#pragma unroll
+    for (int p = 0; p < (8 - SR) * 4; ++p)
+      dma16(wsrc + ((SR * 4 + p) << 10) + lane * 16, wl + ((wave * (8 - SR) * 4 + p) << 10));
+    if (wave < 4) {
+      const int c = 128 * wave + 2 * lane;
+      *reinterpret_cast<float2*>(swl + c) = *reinterpret_cast<const float2*>(g.sw + 512 * t + c);
+      *reinterpret_cast<float2*>(swl + 512 + c) = *reinterpret_cast<const float2*>(g.bias + 512 * t + c);
+    }
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(wr[s][j]));
+  }
+  const int cs = 64 * wave + 16 * gq;
+  const __amdgpu_buffer_rsrc_t orsrc = ws_rsrc(g.out8 + (long)t * g.o8_ts, (long)g.M * g.ldo8);
+  const __amdgpu_buffer_rsrc_t srsrc = ws_rsrc(g.os + (long)t * g.os_ts, 4L * g.M);
+  auto redb = [&](int k) { return red0 + (k & 1) * 8 * WP_R; };
+  auto sa_of = [&](int k) { return g.sa[min(rbk(k) * WP_R + (lane & 31), g.M - 1)]; };
+  auto top_wait = [&]() {
+    // the block's DMA retired (behind it only the previous iteration's 3 stores per wave)
+    __builtin_amdgcn_s_waitcnt(WAIT_VM(3));
+    __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+    __builtin_amdgcn_s_barrier();
+  };
+  // y of block k (acc, row scale sa) and the wave's partial row maxima into red[k & 1]
+  auto form_y = [&](v4i (&acc)[2][4], float sa, float (&y)[2][16], int k) {
+    float sr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      sr[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sa)));
+    float am[2] = {0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 s4 = *reinterpret_cast<const float4*>(swl + cs + 4 * j);
+      const float4 b4 = *reinterpret_cast<const float4*>(swl + 512 + cs + 4 * j);
+      const float swj[4] = {s4.x, s4.y, s4.z, s4.w}, bj[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          y[i][4 * j + e] = ((float)acc[i][j][e] * sr[i]) * swj[e] + bj[e];
+          am[i] = fmaxf(am[i], fabsf(y[i][4 * j + e]));
+        }
+    }
+    float* red = redb(k);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float a = am[i];
+      a = fmaxf(a, __shfl_xor(a, 16));
+      a = fmaxf(a, __shfl_xor(a, 32));
+      red[wave * WP_R + 16 * i + f] = a;
+    }
+  };
+  // the scale of block k's rows (lane: row lane & 31) from red (stored), broadcast per
+  // row fragment: divisor bq, reciprocal iq
+  auto scales = [&](int k, float (&bq)[2], float (&iq)[2]) {
+    const float* red = redb(k);
+    float m = red[lane & 31];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w * WP_R + (lane & 31)]);
+    const float sc = fmaxf(m, 1e-5f) / 127.0f;
+    const float inv = 1.0f / sc;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc), srsrc, 4 * (rbk(k) * WP_R + (lane & 31)), 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      bq[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sc)));
+      iq[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(inv)));
+    }
+  };
+  auto store_row = [&](int k, int i, const uint32_t (&d)[4]) {
+    const long row = rbk(k) * WP_R + 16 * i + f;
+    __builtin_amdgcn_raw_buffer_store_b128(v4u{d[0], d[1], d[2], d[3]}, orsrc, (int)(row * g.ldo8 + cs), 0, 0);
+  };
+  // MFMAs of block k into acc; with q: the quantization of block k-1 (y) between them
+  auto mfma_block = [&](v4i (&acc)[2][4], const uint8_t* cur, bool q, int kq, float (&y)[2][16]) {
+    float bq[2] = {0.0f, 0.0f}, iq[2] = {0.0f, 0.0f};
+    if (q) scales(kq, bq, iq);
+    float last = 0.0f, tq[4];
+    uint32_t d[4];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      v4i a[2], b[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const v4i*>(cur + ((s * 2 + i) << 10) + lane * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = s < SR ? wr[s < SR ? s : 0][j]
+                      : *reinterpret_cast<const v4i*>(wl + (((wave * (8 - SR) + s - SR) * 4 + j) << 10) + lane * 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = s * 8 + i * 4 + j;             // MFMA slot 0..63
+          if (!q || (n & 1) == 0) {
+            if (s == 0) mfma_asm<true>(acc[i][j], b[j], a[i]);
+            else mfma_asm<false>(acc[i][j], b[j], a[i]);
+          } else {
+            // quantized output o of block k-1: row fragment ii, column group jj, element e
+            const int o = n >> 1, ii = o >> 4, jj = (o >> 2) & 3, e = o & 3;
+            float yv = y[ii][4 * jj + e];
+            if (s == 0) mfma_pin<true>(acc[i][j], b[j], a[i], last, yv);
+            else mfma_pin<false>(acc[i][j], b[j], a[i], last, yv);
+            tq[e] = rint_biased(div_cr(yv, bq[ii], iq[ii]));
+            last = tq[e];
+            if (e == 3) {
+              d[jj] = pack4_biased(tq[0], tq[1], tq[2], tq[3]);
+              if (jj == 3) store_row(kq, ii, d);
+            }
+          }
+        }
+    }
+    mfma_settle(acc);
+    if (!q) {           // the 3 stores per iteration the next top wait counts (dropped)
+      const __amdgpu_buffer_rsrc_t nul = ws_rsrc(g.out8, 0L);
+#pragma unroll
+      for (int d2 = 0; d2 < 3; ++d2) __builtin_amdgcn_raw_buffer_store_b32(0u, nul, 0, 0, 0);
+    }
+  };
+
+  v4i acc[2][4];
+  float y[2][16];
+  long long st_top = 0, st_mm = 0, st_y = 0;          // QTX_STAMPS builds only
+  const long long st_0 = QTX_NOW();
+  // ---- block 0: MFMAs, then its y
+  __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
+  __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+  __builtin_amdgcn_s_barrier();
+  float sa = sa_of(0);
+  issue(1);
+  mfma_block(acc, lds, false, 0, y);
+  form_y(acc, sa, y, 0);
+  const long long st_1 = QTX_NOW();
+  // ---- block k: MFMAs with the quantization of block k-1, then the y of block k
+  for (int k = 1; k < nblk; ++k) {
+    const long long t0 = QTX_NOW();
+    top_wait();
+    const long long t1 = QTX_NOW();
+    sa = sa_of(k);
+    issue(k + 1);
+    mfma_block(acc, lds + (k & 1) * WP_STAGE, true, k - 1, y);
+    const long long t2 = QTX_NOW();
+    form_y(acc, sa, y, k);
+    const long long t3 = QTX_NOW();
+    st_top += t1 - t0;
+    st_mm += t2 - t1;
+    st_y += t3 - t2;
+  }
+  QTX_STAMP_VAL(0, st_1 - st_0);
+  QTX_STAMP_VAL(1, st_top);
+  QTX_STAMP_VAL(2, st_mm);
+  QTX_STAMP_VAL(4, st_y);
+  QTX_STAMP_VAL(6, nblk);
+#ifdef QTX_STAMPS
+  // per wave (lane 0 of every wave): top wait, MFMA + quantization, y — after the 16
+  // per-block slots, at [256 * 16 + (block * 8 + wave) * 4 + phase]
+  if (lane == 0 && qtx_stamp_buf) {
+    unsigned long long* pw = qtx_stamp_buf + 256 * 16 + ((long)blockIdx.x * 8 + wave) * 4;
+    pw[0] = st_top; pw[1] = st_mm; pw[2] = st_y; pw[3] = nblk;
+  }
+#endif
+  // ---- the last block's quantization
+  top_wait();
+  {
+    float bq[2], iq[2];
+    scales(nblk - 1, bq, iq);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint32_t d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        d[j] = pack4_biased(rint_biased(div_cr(y[i][4 * j], bq[i], iq[i])),
+                            rint_biased(div_cr(y[i][4 * j + 1], bq[i], iq[i])),
+                            rint_biased(div_cr(y[i][4 * j + 2], bq[i], iq[i])),
+                            rint_biased(div_cr(y[i][4 * j + 3], bq[i], iq[i])));
+      store_row(nblk - 1, i, d);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  QTX_STAMP_VAL(5, QTX_NOW() - st_0);
+}
+
+// =====================================================================================
+// k_gemm_wss: k_gemm_wsq with the two waves of every SIMD in opposite phases.  Stamps of
+// k_gemm_wsq (tools/wsq_stamps.py): the older wave of a SIMD pair (waves 0-3) ends its
+// MFMA phase at ~2450 cycles, its y phase at ~3250, then waits ~1400 at the barrier for
+// the younger one (waves 4-7), whose MFMAs were starved behind it (~3880 cycles): the
+// matrix pipe is busy ~45 % of a block.  Here the groups work in opposite order, so on each
+// SIMD one wave's MFMAs run beside the other wave's VALU-only phase.  Between barriers k
+// and k+1 (interval k):
+//   A (waves 0-3):  M(k);  wait for B's Y(k-1);  Q(k-1);  Y(k)
+//   B (waves 4-7):  Y(k-1);  signal;  M(k) with Q(k-1) interleaved between its MFMAs
+// M = the block's 64 MFMAs per wave, Y = y of a block from its accumulators + the wave's
+// partial row maxima (-> red[j & 1]), Q = quantization of a block with its complete row
+// maxima.  red[j & 1] gets A's partials in interval j and B's in interval j + 1 (before
+// B signals): an LDS counter that every B wave bumps after its Y (monotonic: 4j after
+// interval j's) tells A and the other B waves when block j's maxima are complete.  B keeps
+// a block's accumulators across one barrier; each wave holds one y buffer.
+// =====================================================================================
+__global__ __launch_bounds__(512) void k_gemm_wss(RowGemmArgs g) {
+  constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
+  // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias (4 KB) | red [2][8][32] (2 KB)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4];
+  __shared__ unsigned ydone;                                 // B waves' finished Y phases
+  uint8_t* const wl = lds + 2 * WP_STAGE;
+  float* const swl = reinterpret_cast<float*>(wl + WL);
+  float* const red0 = swl + 1024;                            // [2][8][32]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int f = lane & 15, gq = lane >> 4;
+  const bool grpB = __builtin_amdgcn_readfirstlane(wave) >= 4;
+  const int nsl = g.N >> 9;
+  const int wpt = gridDim.x / nsl;
+  const int t = blockIdx.x % nsl, r0 = blockIdx.x / nsl;
+  const int nb = (g.M + WP_R - 1) / WP_R;
+  if (r0 >= nb) return;
+  const int nblk = (nb - r0 + wpt - 1) / wpt;
+  if (tid == 0) ydone = 0u;
+
+  auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto rbk = [&](int k) { return r0 + min(k, nblk - 1) * wpt; };
+  auto issue = [&](int k) {
+    uint8_t* st = lds + (k & 1) * WP_STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long row = min(rbk(k) * WP_R + 16 * i + f, g.M - 1);
+      dma16(g.A + kp_off(row, 64 * wave + 16 * gq, WS_K), st + ((wave * 2 + i) << 10));
+    }
+  };
+  issue(0);
+  v4i wr[SR][4];
+  {
+    const int8_t* wsrc = g.W + ((long)(t * 8 + wave) << 15);
+    const v4i* ws = reinterpret_cast<const v4i*>(wsrc) + lane;
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wr[s][j] = ws[(s * 4 + j) * 64];
+#pragma unroll
+    for (int p = 0; p < (8 - SR) * 4; ++p)
+      dma16(wsrc + ((SR * 4 + p) << 10) + lane * 16, wl + ((wave * (8 - SR) * 4 + p) << 10));
+    if (wave < 4) {
+      const int c = 128 * wave + 2 * lane;
+      *reinterpret_cast<float2*>(swl + c) = *reinterpret_cast<const float2*>(g.sw + 512 * t + c);
+      *reinterpret_cast<float2*>(swl + 512 + c) = *reinterpret_cast<const float2*>(g.bias + 512 * t + c);
+    }
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(wr[s][j]));
+  }
+  const int cs = 64 * wave + 16 * gq;
+  const __amdgpu_buffer_rsrc_t orsrc = ws_rsrc(g.out8 + (long)t * g.o8_ts, (long)g.M * g.ldo8);
+  const __amdgpu_buffer_rsrc_t srsrc = ws_rsrc(g.os + (long)t * g.os_ts, 4L * g.M);
+  auto redb = [&](int k) { return red0 + (k & 1) * 8 * WP_R; };
+  auto sa_of = [&](int k) { return g.sa[min(rbk(k) * WP_R + (lane & 31), g.M - 1)]; };
+  auto top_wait = [&]() {
+    __builtin_amdgcn_s_waitcnt(WAIT_VM(3));      // behind the block's DMA: 3 stores per wave
+    __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+    __builtin_amdgcn_s_barrier();
+  };
+  auto dummy_stores = [&]() {
+    const __amdgpu_buffer_rsrc_t nul = ws_rsrc(g.out8, 0L);
+#pragma unroll
+    for (int d2 = 0; d2 < 3; ++d2) __builtin_amdgcn_raw_buffer_store_b32(0u, nul, 0, 0, 0);
+  };
+  // B's Y phases of blocks < j all done and visible (bounded: never hang)
+  auto wait_y = [&](int j) {
+#pragma unroll 1
+    for (unsigned spin = 0; spin < (1u << 20); ++spin) {
+      if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&ydone, __ATOMIC_ACQUIRE,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP)) >= 4u * j)
+        break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  // Y: y of block k from acc (row scale sa) and the wave's partial row maxima -> red[k & 1]
+  auto form_y = [&](v4i (&acc)[2][4], float sa, float (&y)[2][16], int k) {
+    float sr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      sr[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sa)));
+    float am[2] = {0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 s4 = *reinterpret_cast<const float4*>(swl + cs + 4 * j);
+      const float4 b4 = *reinterpret_cast<const float4*>(swl + 512 + cs + 4 * j);
+      const float swj[4] = {s4.x, s4.y, s4.z, s4.w}, bj[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          y[i][4 * j + e] = ((float)acc[i][j][e] * sr[i]) * swj[e] + bj[e];
+          am[i] = fmaxf(am[i], fabsf(y[i][4 * j + e]));
+        }
+    }
+    float* red = redb(k);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float a = am[i];
+      a = fmaxf(a, __shfl_xor(a, 16));
+      a = fmaxf(a, __shfl_xor(a, 32));
+      red[wave * WP_R + 16 * i + f] = a;
+    }
+  };
+  auto scales = [&](int k, float (&bq)[2], float (&iq)[2]) {
+    const float* red = redb(k);
+    float m = red[lane & 31];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w * WP_R + (lane & 31)]);
+    const float sc = fmaxf(m, 1e-5f) / 127.0f;
+    const float inv = 1.0f / sc;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc), srsrc, 4 * (rbk(k) * WP_R + (lane & 31)), 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      bq[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sc)));
+      iq[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(inv)));
+    }
+  };
+  auto store_row = [&](int k, int i, const uint32_t (&d)[4]) {
+    const long row = rbk(k) * WP_R + 16 * i + f;
+    __builtin_amdgcn_raw_buffer_store_b128(v4u{d[0], d[1], d[2], d[3]}, orsrc, (int)(row * g.ldo8 + cs), 0, 0);
+  };
+  auto quant_all = [&](int k, const float (&y)[2][16]) {      // 3 stores
+    float bq[2], iq[2];
+    scales(k, bq, iq);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint32_t d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        d[j] = pack4_biased(rint_biased(div_cr(y[i][4 * j], bq[i], iq[i])),
+                            rint_biased(div_cr(y[i][4 * j + 1], bq[i], iq[i])),
+                            rint_biased(div_cr(y[i][4 * j + 2], bq[i], iq[i])),
+                            rint_biased(div_cr(y[i][4 * j + 3], bq[i], iq[i])));
+      store_row(k, i, d);
+    }
+  };
+  // M(k) into acc; Q: with Q(kq) of y between the MFMAs (pinned), 3 stores; else plain
+  auto mfma_block = [&](v4i (&acc)[2][4], int k, auto q_c, int kq, float (&y)[2][16]) {
+    constexpr bool Q = decltype(q_c)::value;
+    const uint8_t* cur = lds + (k & 1) * WP_STAGE;
+    float bq[2] = {0.0f, 0.0f}, iq[2] = {0.0f, 0.0f};
+    if constexpr (Q) scales(kq, bq, iq);
+    float last = 0.0f, tq[4];
+    uint32_t d[4];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      v4i a[2], b[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const v4i*>(cur + ((s * 2 + i) << 10) + lane * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = s < SR ? wr[s < SR ? s : 0][j]
+                      : *reinterpret_cast<const v4i*>(wl + (((wave * (8 - SR) + s - SR) * 4 + j) << 10) + lane * 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = s * 8 + i * 4 + j;
+          if (!Q || (n & 1) == 0) {
+            if (s == 0) mfma_asm<true>(acc[i][j], b[j], a[i]);
+            else mfma_asm<false>(acc[i][j], b[j], a[i]);
+          } else {
+            const int o = n >> 1, ii = o >> 4, jj = (o >> 2) & 3, e = o & 3;
+            float yv = y[ii][4 * jj + e];
+            if (s == 0) mfma_pin<true>(acc[i][j], b[j], a[i], last, yv);
+            else mfma_pin<false>(acc[i][j], b[j], a[i], last, yv);
+            tq[e] = rint_biased(div_cr(yv, bq[ii], iq[ii]));
+            last = tq[e];
+            if (e == 3) {
+              d[jj] = pack4_biased(tq[0], tq[1], tq[2], tq[3]);
+              if (jj == 3) store_row(kq, ii, d);
+            }
+          }
+        }
+    }
+    mfma_settle(acc);
+  };
+  const std::true_type T_{};
+  const std::false_type F_{};
+
+  v4i acc[2][4];
+  float y[2][16];
+  __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
+  __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+  __builtin_amdgcn_s_barrier();
+  float san = sa_of(0);                    // the row scales of this wave's next Y
+  for (int k = 0; k <= nblk; ++k) {
+    if (k > 0) top_wait();
+    const float sac = san;
+    if (!grpB) san = sa_of(k + 1);
+    else if (k < nblk) san = sa_of(k);
+    if (k + 1 < nblk) issue(k + 1);
+    if (!grpB) {
+      if (k < nblk) mfma_block(acc, k, F_, 0, y);
+      if (k >= 1) {
+        wait_y(k);                          // B's partial maxima of block k-1
+        quant_all(k - 1, y);
+      } else {
+        dummy_stores();
+      }
+      if (k < nblk) form_y(acc, sac, y, k);
+    } else {
+      if (k >= 1) {
+        form_y(acc, sac, y, k - 1);
+        if (lane == 0) __hip_atomic_fetch_add(&ydone, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        wait_y(k);                          // every B wave's partials of block k-1
+      }
+      if (k < nblk) {
+        if (k >= 1) mfma_block(acc, k, T_, k - 1, y);
+        else {
+          mfma_block(acc, k, F_, 0, y);
+          dummy_stores();
+        }
+      } else {
+        quant_all(k - 1, y);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // =====================================================================================
@@ -854,7 +1392,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
   };
   auto quant_store = [&](int k, const float (&y)[2][16], float m) {
     const int m0 = rbk(k) * WP_R;
-    const float sc = quant_scale(m, 127.0f);
+    const float sc = fmaxf(m, 1e-5f) / 127.0f;   // true division: branch-free (see k_gemm_wsp)
     const float kk = m < 0x1p37f ? 1.0f : 0x1p-64f;
     const float scs = sc * kk, invs = 1.0f / scs;
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc), srsrc, 4 * (m0 + (lane & 31)), 0, 0);
@@ -983,7 +1521,13 @@ hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {
     if (wpt > nb) wpt = nb;
     const dim3 grid(nsl * wpt), block(512);
     switch (g.epi) {
-      case RE_QUANT: k_gemm_wsp<RE_QUANT><<<grid, block, 0, st>>>(g); break;
+      case RE_QUANT:
+        // k_gemm_wsq (39.6 us at cfg3's M = 32768, profiles/r03b_*) unless QTX_WSQ picks
+        // k_gemm_wsp (0: 45.2 us) or k_gemm_wss (2: 58.7 us, experimental)
+        if (const char* v = getenv("QTX_WSQ"); v && *v == '0') k_gemm_wsp<RE_QUANT><<<grid, block, 0, st>>>(g);
+        else if (v && *v == '2') k_gemm_wss<<<grid, block, 0, st>>>(g);
+        else k_gemm_wsq<<<grid, block, 0, st>>>(g);
+        break;
       case RE_RELU_PMAX:
         // the row-max pass has a light epilogue: all of W fits in registers (no W reads
         // from LDS in the main loop); QTX_WSP_PMAX_SR=5: the LDS-split variant (A/B)

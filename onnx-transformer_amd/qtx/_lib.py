@@ -80,6 +80,7 @@ SIGNATURES = {
     "qtx_pack_w_ws": (I32, [P, I32, I32, P, P]),
     "qtx_pack_int4": (I32, [P, I32, I32, P, P]),
     "qtx_attention_i8": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, P]),
+    "qtx_attention_trace": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, P, P, P]),
     "qtx_attention_i8_quant": (I32, [P, P, P, P, P, P, P, I32, I32, P, P, P]),
     "qtx_skinny_linear": (I32, [I32, P, P, P, I64, P, P, P, I32, P, P, P, I32, I32, I32, I32,
                                 I32, P, P, P, P]),

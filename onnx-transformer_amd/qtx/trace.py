@@ -15,11 +15,18 @@ every QuantLinear MatMul's accumulators under the exported graphs' names:
   (a qtx addition: the graph keeps it in the following Mul).
 * ``MatMul_<n>_out0``  float32(sum_k codes_x * codes_w) of a QuantLinear MatMul (exact
   integer below 2^24), [B, S, N].
+* The attention MatMuls (campaign targets "FirstMatMul" / "SecondMatMul",
+  input/encoder/matmul_3.json): ``MatMul_<QK>_out0`` = float32(sum_d q_codes * k_codes)
+  per head [B, H, Sq, Sk] (the exact integer accumulators, before the / 8 and the mask, as
+  for the QuantLinears); ``Round_<P>_out0`` = rint(P * 127) [B, H, Sq, Sk] (the Round of
+  attention.py:33-35; ``Round_<P>_scale`` = 1/127); ``MatMul_<PV>_out0`` = the per-head
+  context [B, H, Sq, 64] (fp32, the canonical PV chain).
 
 Names follow the campaign target files input/{encoder,decoder}/matmul_*.json (e.g.
 encoder MatMul_6 = Round_42_out0 x Round_4_out0), see :func:`encoder_names` /
-:func:`decoder_names`.  The attention MatMuls' P codes (Round of attention.py:33-35) and
-the QK^T / PV accumulators are not exposed: the attention kernel keeps P on chip.
+:func:`decoder_names`.  The attention intermediates come from qtx_attention_trace (one wave
+per query row and head, the canonical order): its context equals the fused attention's bit
+for bit.
 """
 from __future__ import annotations
 
@@ -146,10 +153,22 @@ class _Tracer:
         self.out[f"Round_{n}_out0"] = w.float().t().contiguous().cpu().numpy()
         self.out[f"Round_{n}_scale"] = _view(torch, sw.value, (N,), "<f4", self.dev).cpu().numpy()
 
-    def attention(self, q, sq, k, sk, v, sv, mask, m_bs, m_is, B, Sq, Sk):
+    def attention(self, q, sq, k, sk, v, sv, mask, m_bs, m_is, B, Sq, Sk, names):
+        """Attention core with its intermediates stored under names = (Round of P,
+        MatMul QK^T, MatMul PV)."""
+        H = 8
         ctx = self.empty(B * Sq, D)
-        _lib.call("qtx_attention_i8", _ptr(q), _ptr(sq), _ptr(k), _ptr(sk), _ptr(v), _ptr(sv),
-                  _ptr(mask), m_bs, m_is, B, 8, Sq, Sk, _ptr(ctx), self.st)
+        qk = self.empty(B, H, Sq, Sk)
+        pc = self.empty(B, H, Sq, Sk)
+        _lib.call("qtx_attention_trace", _ptr(q), _ptr(sq), _ptr(k), _ptr(sk), _ptr(v),
+                  _ptr(sv), _ptr(mask), m_bs, m_is, B, H, Sq, Sk, _ptr(ctx), _ptr(qk), _ptr(pc),
+                  self.st)
+        p_n, qk_n, pv_n = names
+        self.out[f"Round_{p_n}_out0"] = pc.cpu().numpy()
+        self.out[f"Round_{p_n}_scale"] = np.float32(1.0) / np.float32(127.0)
+        self.out[f"MatMul_{qk_n}_out0"] = qk.cpu().numpy()
+        self.out[f"MatMul_{pv_n}_out0"] = (ctx.reshape(B, Sq, H, D // H).permute(0, 2, 1, 3)
+                                           .contiguous().cpu().numpy())
         return ctx
 
 
@@ -186,7 +205,7 @@ def trace_encoder(model, x, src_mask_u8, weights: bool = False):
             q, s = t.quant(y, M, D)
             t.put_codes(act[n.lower()], q, s, shp)
             qkv += [q, s]
-        ctx = t.attention(*qkv, mask, S, 0, B, S, S)
+        ctx = t.attention(*qkv, mask, S, 0, B, S, S, (act["P"], mm["QK"], mm["PV"]))
         cq, cs = t.quant(ctx, M, D)
         t.put_codes(act["ctx"], cq, cs, shp)
         x = t.gemm(cq, cs, t.linear(0, L, 3), M, flags=2, res=x, mm=mm["O"], wname=wt["O"],
@@ -234,7 +253,7 @@ def trace_decoder(model, y, memory, src_mask_u8, tgt_mask_u8, weights: bool = Fa
             q, s = t.quant(yy, M, D)
             t.put_codes(act[n.lower()], q, s, shp)
             qkv += [q, s]
-        ctx = t.attention(*qkv, tm, tm_bs, T, B, T, T)
+        ctx = t.attention(*qkv, tm, tm_bs, T, B, T, T, (act["P"], mm["QK"], mm["PV"]))
         cq, cs = t.quant(ctx, M, D)
         t.put_codes(act["ctx"], cq, cs, shp)
         x = t.gemm(cq, cs, t.linear(1, L, 3), M, flags=2, res=x, mm=mm["O"], wname=wt["O"],
@@ -251,7 +270,7 @@ def trace_decoder(model, y, memory, src_mask_u8, tgt_mask_u8, weights: bool = Fa
             kq, ks = t.quant(yy, Mm, D)
             t.put_codes(act["c_k" if n == "CK" else "c_v"], kq, ks, mshp)
             kv += [kq, ks]
-        ctx = t.attention(q, qs, *kv, sm, S, 0, B, T, S)
+        ctx = t.attention(q, qs, *kv, sm, S, 0, B, T, S, (act["c_P"], mm["CQK"], mm["CPV"]))
         cq, cs = t.quant(ctx, M, D)
         t.put_codes(act["c_ctx"], cq, cs, shp)
         x = t.gemm(cq, cs, t.linear(1, L, 7), M, flags=2, res=x, mm=mm["CO"], wname=wt["CO"],

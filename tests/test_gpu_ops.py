@@ -397,6 +397,35 @@ def test_linear_rows_kp(torch, oracle_model, M):
     np.testing.assert_array_equal(lns.cpu().numpy(), s2)
 
 
+@pytest.mark.parametrize("M,wsq", [(300, 1), (7, 1), (20011, 1), (4096, 1), (4096, 0),
+                                   (300, 2), (7, 2), (20011, 2), (4096, 2), (64, 2)])
+def test_linear_rows_ws_qkv_scales(torch, M, wsq, monkeypatch):
+    """Q/K/V (epi 0, kp = 2) on the weight-stationary kernels (QTX_WSQ=1: k_gemm_wsq, the
+    default, one barrier per block, quantization interleaved between the MFMAs; 0:
+    k_gemm_wsp; 2: k_gemm_wss, the waves of a SIMD in opposite phases) with row
+    scales from 1e-35 to 1e25: outputs from subnormal-tiny (the 1e-5 clamp decides) to
+    ~1e28 (the shared-reciprocal division at every magnitude), bit-exact."""
+    from qtx._lib import lib
+    monkeypatch.setenv("QTX_WSQ", str(wsq))
+    rng = np.random.default_rng(M + 17 * wsq)
+    qx, sx = O.quant_rows(rng.standard_normal((M, 512)).astype(f32))
+    sx = (sx * np.float32(10.0) ** rng.integers(-33, 26, M)).astype(f32)
+    qw, sw = O.quant_weight((rng.standard_normal((1536, 512)) * 0.05).astype(f32), 8)
+    b = (rng.standard_normal(1536) * 1e-3).astype(f32)
+    wk = torch.empty((1536, 512), dtype=torch.int8, device="cuda")
+    assert lib().qtx_pack_w_ws(P(dev(torch, qw)), 1536, 512, P(wk), S0) == 0
+    out8 = torch.empty((3, M, 512), dtype=torch.int8, device="cuda")
+    os_ = torch.empty((3, M), dtype=torch.float32, device="cuda")
+    _rows_call(torch, A=dev(torch, _to_kp(qx)), sa=dev(torch, sx), W=wk, sw=dev(torch, sw),
+               bias=dev(torch, b), M=M, N=1536, K=512, epi=0, out8=out8, ldo8=512,
+               o8_ts=M * 512, os=os_, os_ts=M, kp=2)
+    y = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b)
+    for t in range(3):
+        q, s = O.quant_rows(y[:, 512 * t:512 * (t + 1)])
+        np.testing.assert_array_equal(out8[t].cpu().numpy(), q)
+        np.testing.assert_array_equal(os_[t].cpu().numpy(), s)
+
+
 def _ws_pack_ref(w):
     """The WS order of qtx_pack_w_ws (include/qtx.h), restated in numpy: 1 KB block
     ((t*8 + w)*8 + s)*4 + j, lane l: W[512t + 64w + 16((l & 15) >> 2) + 4j + (l & 3)]
@@ -421,8 +450,9 @@ def test_pack_w_ws(torch):
     assert lib().qtx_pack_w_ws(P(dev(torch, w)), 1024, 256, P(out), S0) != 0   # K != 512
 
 
-@pytest.mark.parametrize("M,nopipe", [(300, 0), (7, 0), (64, 0), (20011, 0), (20011, 1)])
-def test_linear_rows_ws(torch, oracle_model, monkeypatch, M, nopipe):
+@pytest.mark.parametrize("M,nopipe,wsq", [(300, 0, 0), (7, 0, 0), (64, 0, 0), (20011, 0, 0),
+                                          (20011, 1, 0), (300, 0, 1), (20011, 0, 1)])
+def test_linear_rows_ws(torch, oracle_model, monkeypatch, M, nopipe, wsq):
     """kp = 2 (weight-stationary, K = 512): every epilogue bit-exact against the oracle —
     Q/K/V per-token quant (row-major out), FFN1 row maxima + hidden quant (KP out), O-proj
     residual + LayerNorm + quant (KP out) and its fp32 variant; M = 20011 runs several row
@@ -431,6 +461,7 @@ def test_linear_rows_ws(torch, oracle_model, monkeypatch, M, nopipe):
     from qtx._lib import lib
     if nopipe:
         monkeypatch.setenv("QTX_WS_NOPIPE", "1")
+    monkeypatch.setenv("QTX_WSQ", str(wsq))
     rng = np.random.default_rng(M + 7)
 
     def weights(N):

@@ -59,10 +59,14 @@ def run(torch, kw, stream=None):
     assert rc == 0, lib().qtx_last_error()
 
 
-def one_pass(torch, base, stream=None, status=None):
-    h8 = torch.zeros((M, 2048), dtype=torch.int8, device="cuda")
-    sh = torch.empty(M, dtype=torch.float32, device="cuda")
-    gx = torch.empty(((32 * M + 2048) // 4,), dtype=torch.float32, device="cuda")
+def buffers(torch):
+    return (torch.zeros((M, 2048), dtype=torch.int8, device="cuda"),
+            torch.empty(M, dtype=torch.float32, device="cuda"),
+            torch.empty(((32 * M + 2048) // 4,), dtype=torch.float32, device="cuda"))
+
+
+def one_pass(torch, base, stream=None, status=None, bufs=None):
+    h8, sh, gx = bufs if bufs is not None else buffers(torch)
     kw = dict(base, kp=3, pmax_out=gx, out8=h8, ldo8=2048, os=sh)
     if status is not None:
         kw["status"] = status
@@ -82,11 +86,9 @@ def test_concurrent_launches_bit_exact(torch, ffn1):
     the two-pass result bit for bit, and neither raises the timeout flag."""
     base, h_ref, s_ref = ffn1
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    torch.cuda.synchronize()
-    outs = []
-    for _ in range(3):
-        outs.append(one_pass(torch, base, s1))
-        outs.append(one_pass(torch, base, s2))
+    bufs = [buffers(torch) for _ in range(6)]
+    torch.cuda.synchronize()            # the buffers' fills (current stream) are done
+    outs = [one_pass(torch, base, (s1, s2)[i % 2], bufs=b) for i, b in enumerate(bufs)]
     torch.cuda.synchronize()
     for h8, sh, gx in outs:
         np.testing.assert_array_equal(h8.cpu().numpy(), h_ref)

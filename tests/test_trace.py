@@ -74,11 +74,23 @@ def test_traced_encoder_equals_fused_and_oracle(gpu_model, oracle_model):
             acc = np.einsum("bsk,kn->bsn", a.astype(np.float64), w.astype(np.float64))
             np.testing.assert_array_equal(wd[t["output_tensor"]], acc.astype(np.float32))
             n += 1
-        elif t["module"].endswith("FirstMatMul"):    # QK^T: the q and k codes
-            assert wd[t["input_tensor"]].shape == wd[t["weight_tensor"]].shape == (2, 16, 512)
-        else:                                         # PV: the v codes (P stays on chip)
-            assert wd[t["weight_tensor"]].shape == (2, 16, 512)
-    assert n == 12
+        elif t["module"].endswith("FirstMatMul"):    # QK^T: q codes x k codes per head
+            q4 = O.split_heads(wd[t["input_tensor"]], 8).astype(np.float64)
+            k4 = O.split_heads(wd[t["weight_tensor"]], 8).astype(np.float64)
+            acc = np.einsum("bhid,bhjd->bhij", q4, k4)
+            np.testing.assert_array_equal(wd[t["output_tensor"]], acc.astype(np.float32))
+            n += 1
+        else:                                         # PV: P codes x v codes -> the context
+            L = int(t["target_layer"].split("_")[1]) // 8
+            a = T.encoder_names(L)["act"]
+            qr, kr, vr = (f"Round_{a[k]}" for k in ("q", "k", "v"))
+            q4, k4, v4 = (O.split_heads(wd[f"{r}_out0"].astype(np.int8), 8) for r in (qr, kr, vr))
+            sq, sk, sv = (wd[f"{r}_scale"][..., 0] for r in (qr, kr, vr))
+            pc = O.softmax_quant(O.attention_scores(q4, sq, k4, sk, (src != 2)[:, None, :]))
+            np.testing.assert_array_equal(wd[t["input_tensor"]], pc.astype(np.float32))
+            np.testing.assert_array_equal(wd[t["output_tensor"]], O.attention_pv(pc, v4, sv))
+            n += 1
+    assert n == 24
 
 
 @pytest.mark.gpu
@@ -101,6 +113,20 @@ def test_traced_decoder_equals_fused(gpu_model, oracle_model):
                 "MatMul_19", "MatMul_31"):           # cross QK^T: q codes x memory K codes
             assert wd[t["input_tensor"]].shape == (2, 5, 512)
             assert wd[t["weight_tensor"]].shape == (2, 12, 512)
+            q4 = O.split_heads(wd[t["input_tensor"]], 8).astype(np.float64)
+            k4 = O.split_heads(wd[t["weight_tensor"]], 8).astype(np.float64)
+            np.testing.assert_array_equal(wd[t["output_tensor"]],
+                                          np.einsum("bhid,bhjd->bhij", q4, k4).astype(np.float32))
+    # every attention MatMul of every layer is stored by name: self QK^T [B,H,T,T], cross
+    # P codes [B,H,T,S], self / cross PV contexts per head
+    for L in range(6):
+        nm = T.decoder_names(L)
+        mm, a = nm["matmul"], nm["act"]
+        assert wd[f"MatMul_{mm['QK']}_out0"].shape == (2, 8, 5, 5)
+        assert wd[f"Round_{a['c_P']}_out0"].shape == (2, 8, 5, 12)
+        assert wd[f"MatMul_{mm['PV']}_out0"].shape == wd[f"MatMul_{mm['CPV']}_out0"].shape == (2, 8, 5, 64)
+        # causal mask: P of a future key is 0
+        assert (wd[f"Round_{a['P']}_out0"][:, :, 0, 1:] == 0).all()
 
 
 @pytest.mark.gpu
