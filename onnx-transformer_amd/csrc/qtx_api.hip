@@ -1478,11 +1478,6 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
     return greedy_step_fused(m, gv[i], gr.rows(i, B), S, max_len, ids + (long)gr.b0(i) * max_len,
                              src_mask + (long)gr.b0(i) * S, s);
   };
-  if (env_flag("QTX_NO_GRAPH")) {
-    for (int t = 0; t + 1 < max_len; ++t)
-      for (int i = 0; i < gr.G; ++i) RC(step_fn(i, st));
-    return QTX_OK;
-  }
   // One decode step per sub-batch captured once per (shape, buffers) as a hipGraph on its
   // own stream and replayed max_len-1 times there; the streams fork from and join back
   // into the caller's stream.
@@ -1495,14 +1490,30 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
       HIPCHK(hipStreamCreateWithFlags(&mm->gstream[i], hipStreamNonBlocking));
       HIPCHK(hipEventCreateWithFlags(&mm->ev_out[i], hipEventDisableTiming));
     }
+  if (env_flag("QTX_NO_GRAPH")) {     // eager launches (diagnostic); sub-batches on their streams
+    const bool fk = gr.G > 1;
+    if (fk) {
+      HIPCHK(hipEventRecord(mm->ev_in, st));
+      for (int i = 0; i < gr.G; ++i) HIPCHK(hipStreamWaitEvent(mm->gstream[i], mm->ev_in, 0));
+    }
+    for (int t = 0; t + 1 < max_len; ++t)
+      for (int i = 0; i < gr.G; ++i) RC(step_fn(i, fk ? mm->gstream[i] : st));
+    if (fk)
+      for (int i = 0; i < gr.G; ++i) {
+        HIPCHK(hipEventRecord(mm->ev_out[i], mm->gstream[i]));
+        HIPCHK(hipStreamWaitEvent(st, mm->ev_out[i], 0));
+      }
+    return QTX_OK;
+  }
   // steps per graph: the whole decode in one graph by default (one graph launch); must
   // divide max_len-1 (the step position is read from device memory, so replays chain)
   int per_graph = max_len - 1;
   if (const char* v = getenv("QTX_GRAPH_STEPS"))
     if (*v && atoi(v) > 0 && (max_len - 1) % atoi(v) == 0) per_graph = atoi(v);
   if (max_len <= 1) return QTX_OK;
+  const bool joint = gr.G > 1 && env_flag("QTX_GROUP_GRAPH");
   std::string variant;
-  for (const char* k : {"QTX_SPLIT_LN", "QTX_FFN_QKERNEL", "QTX_ABLATE", "QTX_ABLATE_NOP"}) {
+  for (const char* k : {"QTX_SPLIT_LN", "QTX_FFN_QKERNEL", "QTX_ABLATE", "QTX_ABLATE_NOP", "QTX_GROUP_GRAPH"}) {
     const char* v = getenv(k);
     variant += std::string(k) + "=" + (v ? v : "") + ";";
   }
@@ -1514,7 +1525,34 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
     auto drop = [&] {
       for (hipGraphExec_t e : execs) (void)hipGraphExecDestroy(e);
     };
-    for (int i = 0; i < gr.G; ++i) {
+    // QTX_GROUP_GRAPH (experiment): the G sub-batches as G independent branches of ONE graph
+    // (forked and joined inside the capture), launched on the caller's stream
+    if (joint) {
+      hipGraph_t graph = nullptr;
+      hipStream_t s0 = mm->gstream[0];
+      HIPCHK(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
+      int rc = QTX_OK;
+      hipError_t e = hipEventRecord(mm->ev_in, s0);
+      for (int i = 1; i < gr.G && e == hipSuccess; ++i) e = hipStreamWaitEvent(mm->gstream[i], mm->ev_in, 0);
+      for (int t = 0; t < per_graph && rc == QTX_OK && e == hipSuccess; ++t)
+        for (int i = 0; i < gr.G && rc == QTX_OK; ++i) rc = step_fn(i, mm->gstream[i]);
+      for (int i = 1; i < gr.G && e == hipSuccess; ++i) {
+        e = hipEventRecord(mm->ev_out[i], mm->gstream[i]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s0, mm->ev_out[i], 0);
+      }
+      const hipError_t e2 = hipStreamEndCapture(s0, &graph);
+      if (rc != QTX_OK || e != hipSuccess || e2 != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        if (rc != QTX_OK) return rc;
+        HIPCHK(e != hipSuccess ? e : e2);
+      }
+      hipGraphExec_t exec = nullptr;
+      e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      HIPCHK(e);
+      execs.push_back(exec);
+    }
+    for (int i = 0; i < (joint ? 0 : gr.G); ++i) {
       hipGraph_t graph = nullptr;
       hipError_t e = hipStreamBeginCapture(mm->gstream[i], hipStreamCaptureModeThreadLocal);
       if (e != hipSuccess) { drop(); HIPCHK(e); }
@@ -1537,9 +1575,10 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
     ent.execs = std::move(execs);
     it = mm->graphs.emplace(key, std::move(ent)).first;
   }
-  // One sub-batch: replay on the caller's stream itself (a graph captured on one stream can
-  // be launched on any).  Several: fork to the model's streams and join back.
-  const bool fork = gr.G > 1;
+  // One sub-batch (or one joint graph): replay on the caller's stream itself (a graph
+  // captured on one stream can be launched on any).  Several: fork to the model's streams
+  // and join back.
+  const bool fork = gr.G > 1 && !joint;
   hipStream_t ls[QTX_MAX_GROUPS];
   for (int i = 0; i < gr.G; ++i) ls[i] = fork ? mm->gstream[i] : st;
   if (fork) {
@@ -1554,7 +1593,7 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
     HIPCHK(hipEventRecord(tg0, ls[0]));
   }
   for (int t = 0; t < (max_len - 1) / per_graph; ++t)
-    for (int i = 0; i < gr.G; ++i) HIPCHK(hipGraphLaunch(it->second.execs[i], ls[i]));
+    for (int i = 0; i < (int)it->second.execs.size(); ++i) HIPCHK(hipGraphLaunch(it->second.execs[i], ls[i]));
   if (time_graph) {
     float ms = 0.0f;
     HIPCHK(hipEventRecord(tg1, ls[0]));

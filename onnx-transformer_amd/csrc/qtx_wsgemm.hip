@@ -1482,6 +1482,276 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// =====================================================================================
+// k_gemm_wsy: the one-pass FFN1 of k_gemm_wsx with k_gemm_wsq's schedule — ONE barrier per
+// 32-row block and the quantization between the MFMAs (asm statements, pinned):
+//   iteration k:  top barrier (block k-1's partial row maxima complete in red[(k-1) & 1]);
+//                 the row maxima of block k-2 over all 4 slices (the partners published
+//                 them an iteration ago); block k-1's slice maxima published; block k+1's
+//                 A by LDS-DMA; the 64 MFMAs of block k with block k-2's quantized outputs
+//                 pinned between them; y = relu(((acc * sa) * sw) + b) of block k and its
+//                 partial row maxima -> red[k & 1] (VALU-only phase).
+// y of blocks k-1 and k-2 are both held (one buffer per block parity): the quantization of
+// block k waits two iterations for its partners' maxima, so the hand-off latency hides under
+// a whole iteration as in k_gemm_wsx.  The exchange (tickets, granules, bounded waits that
+// report DEV_E_EXCHANGE_TIMEOUT) is k_gemm_wsx's.  Numerics as k_gemm_wsq: RN(y / s) by
+// div_cr with the row's reciprocal, s by true division.
+// Wait ordering: vmcnt counts loads and stores in order, so the granule loads (which are
+// waited for at once) go before this iteration's DMA and stores, behind only the previous
+// iteration's stores; every iteration issues 3 stores after its DMA (dropped ones where
+// there is nothing to store) for the vmcnt(3) at the next top.
+// =====================================================================================
+__global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
+  constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
+  // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias (4 KB) | red [2][8][32] (2 KB)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4];
+  uint8_t* const wl = lds + 2 * WP_STAGE;
+  float* const swl = reinterpret_cast<float*>(wl + WL);
+  float* const red0 = swl + 1024;                            // [2][8][32]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int f = lane & 15, gq = lane >> 4;
+  const int nb = (g.M + WP_R - 1) / WP_R;
+  unsigned long long* const gran = reinterpret_cast<unsigned long long*>(g.pmax_out);
+  __shared__ int ticket;
+  if (tid == 0)
+    ticket = (int)atomicAdd(reinterpret_cast<unsigned*>(gran + 4L * 32 * nb), 1u);
+  __syncthreads();
+  const int q = ticket, wpt = gridDim.x >> 2;       // tickets as in k_gemm_wsx
+  const int t = (q >> 3) & 3, r0 = (q & 7) + 8 * (q >> 5);
+  if (r0 >= nb) return;
+  const int nblk = (nb - r0 + wpt - 1) / wpt;
+
+  auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto rbk = [&](int k) { return r0 + min(k, nblk - 1) * wpt; };
+  auto issue = [&](int k) {
+    uint8_t* st = lds + (k & 1) * WP_STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long row = min(rbk(k) * WP_R + 16 * i + f, g.M - 1);
+      dma16(g.A + kp_off(row, 64 * wave + 16 * gq, WS_K), st + ((wave * 2 + i) << 10));
+    }
+  };
+  issue(0);
+  v4i wr[SR][4];
+  {
+    const int8_t* wsrc = g.W + ((long)(t * 8 + wave) << 15);
+    const v4i* ws = reinterpret_cast<const v4i*>(wsrc) + lane;
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wr[s][j] = ws[(s * 4 + j) * 64];
+#pragma unroll
+    for (int p = 0; p < (8 - SR) * 4; ++p)
+      dma16(wsrc + ((SR * 4 + p) << 10) + lane * 16, wl + ((wave * (8 - SR) * 4 + p) << 10));
+    if (wave < 4) {
+      const int c = 128 * wave + 2 * lane;
+      *reinterpret_cast<float2*>(swl + c) = *reinterpret_cast<const float2*>(g.sw + 512 * t + c);
+      *reinterpret_cast<float2*>(swl + 512 + c) = *reinterpret_cast<const float2*>(g.bias + 512 * t + c);
+    }
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(wr[s][j]));
+  }
+  const int cs = 64 * wave + 16 * gq;
+  const int c0 = 512 * t + cs;
+  const __amdgpu_buffer_rsrc_t orsrc = ws_rsrc(g.out8, (long)(g.M + (g.M & 1)) * g.ldo8);
+  const __amdgpu_buffer_rsrc_t srsrc = ws_rsrc(g.os, t == 0 ? 4L * g.M : 0L);
+  auto redb = [&](int k) { return red0 + (k & 1) * 8 * WP_R; };
+  auto sa_of = [&](int k) { return g.sa[min(rbk(k) * WP_R + (lane & 31), g.M - 1)]; };
+  auto dummy_stores = [&]() {
+    const __amdgpu_buffer_rsrc_t nul = ws_rsrc(g.out8, 0L);
+#pragma unroll
+    for (int d2 = 0; d2 < 3; ++d2) __builtin_amdgcn_raw_buffer_store_b32(0u, nul, 0, 0, 0);
+  };
+  // Y: y of block k (ReLU) from acc and the wave's partial row maxima -> red[k & 1]
+  auto form_y = [&](v4i (&acc)[2][4], float sa, float (&y)[2][16], int k) {
+    float sr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      sr[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sa)));
+    float am[2] = {0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 s4 = *reinterpret_cast<const float4*>(swl + cs + 4 * j);
+      const float4 b4 = *reinterpret_cast<const float4*>(swl + 512 + cs + 4 * j);
+      const float swj[4] = {s4.x, s4.y, s4.z, s4.w}, bj[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          y[i][4 * j + e] = fmaxf(((float)acc[i][j][e] * sr[i]) * swj[e] + bj[e], 0.0f);
+          am[i] = fmaxf(am[i], y[i][4 * j + e]);
+        }
+    }
+    float* red = redb(k);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float a = am[i];
+      a = fmaxf(a, __shfl_xor(a, 16));
+      a = fmaxf(a, __shfl_xor(a, 32));
+      red[wave * WP_R + 16 * i + f] = a;
+    }
+  };
+  auto slice_max = [&](int k) {
+    const float* red = redb(k);
+    float m = red[lane & 31];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w * WP_R + (lane & 31)]);
+    return m;
+  };
+  auto gidx = [&](int rb, int tt) { return ((long)rb * 4 + tt) * 32 + (lane & 31); };
+  auto publish = [&](int k, float m) {
+    if (wave == 0 && lane < 32)
+      __hip_atomic_store(gran + gidx(rbk(k), t), (1ull << 32) | __float_as_uint(m),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  const unsigned lim = (unsigned)g.spin_limit;
+  auto full_max = [&](int k, float mloc) {
+    const int rb = rbk(k);
+    float m = mloc;
+    for (unsigned spin = 0;; ++spin) {
+      bool ok = true;
+      float mx = mloc;
+#pragma unroll
+      for (int d = 1; d < 4; ++d) {
+        const unsigned long long v = __hip_atomic_load(gran + gidx(rb, (t + d) & 3), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        ok &= (v >> 32) == 1ull;
+        mx = fmaxf(mx, __uint_as_float((unsigned)v));
+      }
+      if (__all(ok)) { m = mx; break; }
+      if (spin >= lim) {                            // bounded: never hang, never silent
+        if (lane == 0)
+          __hip_atomic_fetch_or(g.status, DEV_E_EXCHANGE_TIMEOUT, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    return m;
+  };
+  // block k's scale from its full row maximum m (stored; lane: row lane & 31), broadcast per
+  // row fragment: divisor bq, reciprocal iq
+  auto scales = [&](int k, float m, float (&bq)[2], float (&iq)[2]) {
+    const float sc = fmaxf(m, 1e-5f) / 127.0f;
+    const float inv = 1.0f / sc;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc), srsrc, 4 * (rbk(k) * WP_R + (lane & 31)), 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      bq[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sc)));
+      iq[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(inv)));
+    }
+  };
+  auto store_row = [&](int k, int i, const uint32_t (&d)[4]) {
+    const long row = rbk(k) * WP_R + 16 * i + f;
+    __builtin_amdgcn_raw_buffer_store_b128(v4u{d[0], d[1], d[2], d[3]}, orsrc, (int)kp_off(row, c0, g.ldo8), 0, 0);
+  };
+  auto quant_all = [&](int k, const float (&y)[2][16], float m) {      // 3 stores
+    float bq[2], iq[2];
+    scales(k, m, bq, iq);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint32_t d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        d[j] = pack4_biased(rint_biased(div_cr(y[i][4 * j], bq[i], iq[i])),
+                            rint_biased(div_cr(y[i][4 * j + 1], bq[i], iq[i])),
+                            rint_biased(div_cr(y[i][4 * j + 2], bq[i], iq[i])),
+                            rint_biased(div_cr(y[i][4 * j + 3], bq[i], iq[i])));
+      store_row(k, i, d);
+    }
+  };
+  // M(k) into acc; Q: block kq's quantization (y, full maximum m) pinned between the MFMAs
+  auto mfma_block = [&](v4i (&acc)[2][4], int k, auto q_c, int kq, float (&y)[2][16], float m) {
+    constexpr bool Q = decltype(q_c)::value;
+    const uint8_t* cur = lds + (k & 1) * WP_STAGE;
+    float bq[2] = {0.0f, 0.0f}, iq[2] = {0.0f, 0.0f};
+    if constexpr (Q) scales(kq, m, bq, iq);
+    float last = 0.0f, tq[4];
+    uint32_t d[4];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      v4i a[2], b[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const v4i*>(cur + ((s * 2 + i) << 10) + lane * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = s < SR ? wr[s < SR ? s : 0][j]
+                      : *reinterpret_cast<const v4i*>(wl + (((wave * (8 - SR) + s - SR) * 4 + j) << 10) + lane * 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = s * 8 + i * 4 + j;
+          if (!Q || (n & 1) == 0) {
+            if (s == 0) mfma_asm<true>(acc[i][j], b[j], a[i]);
+            else mfma_asm<false>(acc[i][j], b[j], a[i]);
+          } else {
+            const int o = n >> 1, ii = o >> 4, jj = (o >> 2) & 3, e = o & 3;
+            float yv = y[ii][4 * jj + e];
+            if (s == 0) mfma_pin<true>(acc[i][j], b[j], a[i], last, yv);
+            else mfma_pin<false>(acc[i][j], b[j], a[i], last, yv);
+            tq[e] = rint_biased(div_cr(yv, bq[ii], iq[ii]));
+            last = tq[e];
+            if (e == 3) {
+              d[jj] = pack4_biased(tq[0], tq[1], tq[2], tq[3]);
+              if (jj == 3) store_row(kq, ii, d);
+            }
+          }
+        }
+    }
+    mfma_settle(acc);
+    if constexpr (!Q) dummy_stores();
+  };
+  const std::true_type T_{};
+  const std::false_type F_{};
+
+  v4i acc[2][4];
+  float y0[2][16], y1[2][16];      // y of the even / odd blocks
+  float mq0 = 0.0f, mq1 = 0.0f;    // their slice maxima
+  __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
+  __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+  __builtin_amdgcn_s_barrier();
+  // iteration k; yb / mb: the buffers of blocks of k's parity (block k-2 in, block k out),
+  // mo: the slice maximum of block k-1 (the other parity)
+  auto iter = [&](int k, float (&yb)[2][16], float& mb, float& mo) {
+    if (k > 0) {
+      __builtin_amdgcn_s_waitcnt(WAIT_VM(3));   // block k's DMA retired (behind: 3 stores)
+      __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+      __builtin_amdgcn_s_barrier();
+    }
+    float m2 = 0.0f;
+    if (k >= 2) m2 = full_max(k - 2, mb);       // granule loads: before this iteration's DMA
+    const float sa = sa_of(k);
+    if (k >= 1 && k <= nblk) {
+      mo = slice_max(k - 1);
+      publish(k - 1, mo);
+    }
+    if (k + 1 < nblk) issue(k + 1);
+    if (k < nblk) {
+      if (k >= 2) mfma_block(acc, k, T_, k - 2, yb, m2);
+      else mfma_block(acc, k, F_, 0, yb, 0.0f);
+      form_y(acc, sa, yb, k);
+    } else if (k >= 2) {
+      quant_all(k - 2, yb, m2);
+    } else {
+      dummy_stores();
+    }
+  };
+  for (int k = 0; k <= nblk + 1; k += 2) {
+    iter(k, y0, mq0, mq1);
+    if (k + 1 <= nblk + 1) iter(k + 1, y1, mq1, mq0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 hipError_t launch_gemm_wsx(const RowGemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return hipSuccess;
   if (g.K != WS_K || g.N != 2048 || g.epi != RE_RELU_QUANT_PMAX || g.fault.kind != FK_NONE ||
@@ -1505,7 +1775,9 @@ hipError_t launch_gemm_wsx(const RowGemmArgs& g, hipStream_t st) {
     a.spin_limit = v && *v ? atoi(v) : (1 << 18);
     if (a.spin_limit < 0) a.spin_limit = 0;
   }
-  k_gemm_wsx<<<dim3(4 * 8 * ng), dim3(512), 0, st>>>(a);
+  // k_gemm_wsy (MFMA-interleaved quantization) unless QTX_WSY=0 picks k_gemm_wsx
+  if (const char* v = getenv("QTX_WSY"); v && *v == '0') k_gemm_wsx<<<dim3(4 * 8 * ng), dim3(512), 0, st>>>(a);
+  else k_gemm_wsy<<<dim3(4 * 8 * ng), dim3(512), 0, st>>>(a);
   return hipGetLastError();
 }
 

@@ -1,4 +1,4 @@
-"""The weight-stationary Q/K/V kernels issue their MFMAs as asm statements (qtx_wsgemm.hip
+"""The weight-stationary Q/K/V and one-pass FFN1 kernels issue their MFMAs as asm statements (qtx_wsgemm.hip
 mfma_asm / mfma_pin), so the compiler inserts none of the wait states MFMA results need
 before other instructions touch them: k_gemm_wss once read accumulators 13-17 wait states
 after their MFMA (copies at its loop latch), 0.5-5 % of Q/K/V outputs wrong.  Compiles the
@@ -22,6 +22,7 @@ def test_asm_mfma_wait_states(tmp_path):
                     "-fno-fast-math", "--cuda-device-only", "-S", "-o", str(out), src],
                    check=True, capture_output=True, timeout=600)
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools/check_asm_mfma.py"), str(out),
-                        "k_gemm_wsq", "k_gemm_wss"], capture_output=True, text=True, timeout=120)
+                        "k_gemm_wsq", "k_gemm_wss", "k_gemm_wsy"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-3000:]
-    assert "k_gemm_wsq: 0 hazards" in r.stdout and "k_gemm_wss: 0 hazards" in r.stdout
+    for k in ("k_gemm_wsq", "k_gemm_wss", "k_gemm_wsy"):
+        assert f"{k}: 0 hazards" in r.stdout

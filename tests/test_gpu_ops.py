@@ -426,6 +426,36 @@ def test_linear_rows_ws_qkv_scales(torch, M, wsq, monkeypatch):
         np.testing.assert_array_equal(os_[t].cpu().numpy(), s)
 
 
+@pytest.mark.parametrize("M,wsy", [(300, 1), (7, 1), (20011, 1), (4096, 1), (4096, 0), (64, 1)])
+def test_linear_rows_ws_ffn1_onepass_scales(torch, M, wsy, monkeypatch):
+    """FFN1 in one pass (kp = 3: ReLU + per-token quantization over all 2048 columns, the
+    4 column slices' row maxima exchanged inside the launch) on k_gemm_wsy (QTX_WSY=1, the
+    default: quantization between the MFMAs) and k_gemm_wsx (0), with row scales from
+    1e-35 to 1e25; bit-exact, and the exchange never timed out (status word 0)."""
+    from qtx._lib import lib
+    monkeypatch.setenv("QTX_WSY", str(wsy))
+    rng = np.random.default_rng(M + 31 * wsy)
+    qx, sx = O.quant_rows(rng.standard_normal((M, 512)).astype(f32))
+    sx = (sx * np.float32(10.0) ** rng.integers(-33, 26, M)).astype(f32)
+    qw, sw = O.quant_weight((rng.standard_normal((2048, 512)) * 0.05).astype(f32), 8)
+    b = (rng.standard_normal(2048) * 1e-3).astype(f32)
+    wk = torch.empty((2048, 512), dtype=torch.int8, device="cuda")
+    assert lib().qtx_pack_w_ws(P(dev(torch, qw)), 2048, 512, P(wk), S0) == 0
+    h8 = torch.zeros((M + (M & 1), 2048), dtype=torch.int8, device="cuda")
+    sh = torch.full((M,), -1.0, dtype=torch.float32, device="cuda")
+    nb = (M + 31) // 32
+    gx = torch.empty(((32 * M + 2048) // 4,), dtype=torch.float32, device="cuda")
+    _rows_call(torch, A=dev(torch, _to_kp(qx)), sa=dev(torch, sx), W=wk, sw=dev(torch, sw),
+               bias=dev(torch, b), M=M, N=2048, K=512, kp=3, epi=3, pmax_out=gx, out8=h8,
+               ldo8=2048, os=sh)
+    h = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b, relu=True)
+    qh, s = O.quant_rows(h)
+    np.testing.assert_array_equal(_from_kp(h8.cpu().numpy(), M), qh)
+    np.testing.assert_array_equal(sh.cpu().numpy(), s)
+    status = gx.view(torch.int32)[2 * (4 * 32 * nb) + 1].item()
+    assert status == 0
+
+
 def _ws_pack_ref(w):
     """The WS order of qtx_pack_w_ws (include/qtx.h), restated in numpy: 1 KB block
     ((t*8 + w)*8 + s)*4 + j, lane l: W[512t + 64w + 16((l & 15) >> 2) + 4j + (l & 3)]
