@@ -48,6 +48,7 @@ class Codes:
         self.idx, self.val, self.crc, self.size = [], [], [], []
         self.flips, self.ties = [], []
         self._quant_rows, self._softmax_quant = O.quant_rows, O.softmax_quant
+        self._saved = (O.quant_rows, O.softmax_quant)      # what __exit__ puts back
 
     @property
     def n_calls(self):
@@ -111,7 +112,7 @@ class Codes:
         return self
 
     def __exit__(self, *exc):
-        O.quant_rows, O.softmax_quant = self._quant_rows, self._softmax_quant
+        O.quant_rows, O.softmax_quant = self._saved
 
 
 def enc_layer(om, lp, y, m):
