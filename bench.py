@@ -194,6 +194,9 @@ def _quantized_rows(rng, M, K, relu=False):
     return np.rint(g / s).astype(np.int8)
 
 
+WS_RES_MAX_M = 8192       # qtx_api.hip ws_res_ok: O-projection weight-stationary below this M
+
+
 def time_row_gemms(M=256 * 128, reps=10, ws=True, operands="encoder"):
     """The five QuantLinear launches of one cfg3 encoder layer through qtx_linear_rows on
     synthetic int8 operands (QKV + per-token quant, O + residual + LN + quant, FFN1 row-max
@@ -234,7 +237,10 @@ def time_row_gemms(M=256 * 128, reps=10, ws=True, operands="encoder"):
     kps = {}
     for (N, K), w in list(W.items()):
         wk = torch.empty_like(w)
-        kps[(N, K)] = 2 if (ws and K == D and N != D) else 1   # Q/K/V and FFN1 (qtx_api.hip qws)
+        # Q/K/V and FFN1 weight-stationary (qtx_api.hip rowgemm); O too below the M bound of
+        # qtx_api.hip ws_res_ok (the same environment override, the same default)
+        o_ws = 2048 <= M < int(os.environ.get("QTX_WS_RES_MAX_M", str(WS_RES_MAX_M)))
+        kps[(N, K)] = 2 if (ws and K == D and (N != D or o_ws)) else 1
         _lib.call("qtx_pack_w_ws" if kps[(N, K)] == 2 else "qtx_pack_w_kp", C.c_void_p(w.data_ptr()),
                   N, K, C.c_void_p(wk.data_ptr()), C.c_void_p(torch.cuda.current_stream().cuda_stream))
         W[(N, K)] = wk

@@ -991,18 +991,18 @@ struct GreedyWS {
 
 // Sub-batch split of the fused decode.  Sentences are independent (per-token quantization:
 // no value depends on another sentence), and one sub-batch's step is a chain of ~50
-// latency-bound kernels that each occupy a fraction of the 256 CUs.  In one process the
-// G sub-batch graphs on G streams measured slower than one graph, not overlapped (B = 32:
-// 16.2 / 21.6 ms for G = 1 / 2; B = 128: 23.4 / 26.9; B = 256: 35.1 / 35.7): the groups
-// overlap only partly, and one graph over the whole batch is at least as fast.
-// Default G = 1; QTX_DECODE_GROUPS overrides it (experiments).
+// latency-bound kernels that each occupy a fraction of the 256 CUs.  G sub-batch graphs
+// on G streams (ms per decode, profiles/r03_concurrency.md): B = 32: 14.5 / 21.0 for
+// G = 1 / 2; B = 256: 34.9 / 35.8; B = 512: 59.0 / 51.9 — two chains of 256 rows overlap
+// as well as two processes of 256 sentences each (50.6), two of 128 or 16 do not gain.
+// Default G = 2 from B = 512, else 1; QTX_DECODE_GROUPS overrides it (experiments).
 struct Groups {
   int G, Bg;   // G groups of Bg rows (the last one may be shorter)
   int b0(int i) const { return i * Bg; }
   int rows(int i, int B) const { return std::min(B, (i + 1) * Bg) - i * Bg; }
 };
 Groups decode_groups(int B) {
-  int G = 1;   // measured: concurrent sub-batch graphs on extra HW queues run slower
+  int G = B >= 512 ? 2 : 1;
   if (const char* v = getenv("QTX_DECODE_GROUPS"))
     if (*v) G = atoi(v);
   G = std::max(1, std::min(std::min(G, QTX_MAX_GROUPS), B));

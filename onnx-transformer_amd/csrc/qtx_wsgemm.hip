@@ -1752,6 +1752,184 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// =====================================================================================
+// k_gemm_wsr: the O-projection (RE_RES_LN, K = N = 512) weight-stationary at large M:
+// x = res + y, x stored, the next LayerNorm in the canonical order and its per-token
+// quantization (KP out) — sublayer_connection.py:15-17, layer_norm.py:12-15,
+// quant_linear.py:30-43.  The launch is bound by HBM (per 32-row block: 64 KB of residual
+// in, 64 KB of x and 16 KB of codes out, against 2,048 MFMA cycles per SIMD), so the design
+// keeps HBM busy: 32-row blocks (4 per workgroup at cfg3's M), two A stages (block k+1's
+// DMA under block k), block k's residual rows loaded at the top of its iteration (their
+// latency hides under the MFMAs), and every store unconditional (buffer range check), so
+// the next top waits with a counted vmcnt instead of draining the stores.
+// Epilogue in 4 rounds of 8 rows: the lanes holding those rows stage y in the block's A
+// stage (free once every wave is past its MFMAs; 16 KB = 8 rows x 512 fp32, chunk c of row
+// r at c ^ (r & 7)), then wave w takes row w of the round whole (ln_rows512 / quant_rows512
+// need a row's 512 values in the canonical lane layout).
+// =====================================================================================
+__global__ __launch_bounds__(512) void k_gemm_wsr(RowGemmArgs g) {
+  constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
+  // LDS: 2 A stages (32 KB; the consumed one stages y) | W K steps 5-7 (96 KB) | sw, bias
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096];
+  uint8_t* const wl = lds + 2 * WP_STAGE;
+  float* const swl = reinterpret_cast<float*>(wl + WL);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int f = lane & 15, gq = lane >> 4;
+  const int wpt = gridDim.x;
+  const int r0 = blockIdx.x;
+  const int nb = (g.M + WP_R - 1) / WP_R;
+  if (r0 >= nb) return;
+  const int nblk = (nb - r0 + wpt - 1) / wpt;
+
+  auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto rbk = [&](int k) { return r0 + min(k, nblk - 1) * wpt; };
+  auto issue = [&](int k) {
+    uint8_t* st = lds + (k & 1) * WP_STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long row = min(rbk(k) * WP_R + 16 * i + f, g.M - 1);
+      dma16(g.A + kp_off(row, 64 * wave + 16 * gq, WS_K), st + ((wave * 2 + i) << 10));
+    }
+  };
+  issue(0);
+  v4i wr[SR][4];
+  {
+    const int8_t* wsrc = g.W + ((long)wave << 15);
+    const v4i* ws = reinterpret_cast<const v4i*>(wsrc) + lane;
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wr[s][j] = ws[(s * 4 + j) * 64];
+#pragma unroll
+    for (int p = 0; p < (8 - SR) * 4; ++p)
+      dma16(wsrc + ((SR * 4 + p) << 10) + lane * 16, wl + ((wave * (8 - SR) * 4 + p) << 10));
+    if (wave < 4) {
+      const int c = 128 * wave + 2 * lane;
+      *reinterpret_cast<float2*>(swl + c) = *reinterpret_cast<const float2*>(g.sw + c);
+      *reinterpret_cast<float2*>(swl + 512 + c) = *reinterpret_cast<const float2*>(g.bias + c);
+    }
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(wr[s][j]));
+  }
+  const int cs = 64 * wave + 16 * gq;
+  float ga[2][4], gb[2][4];
+  ln_params512(g.ln_a, g.ln_b, lane, ga, gb);
+  const __amdgpu_buffer_rsrc_t xrsrc = ws_rsrc(g.xout, 4L * 512 * g.M);
+  const __amdgpu_buffer_rsrc_t qrsrc = ws_rsrc(g.lnq, (long)(g.M + (g.M & 1)) * 512);
+  const __amdgpu_buffer_rsrc_t srsrc = ws_rsrc(g.lns, 4L * g.M);
+
+  __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
+  __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+  __builtin_amdgcn_s_barrier();
+  for (int k = 0; k < nblk; ++k) {
+    if (k > 0) {
+      // block k's DMA retired: behind it only block k-1's 20 stores (4 rounds x 5)
+      __builtin_amdgcn_s_waitcnt(WAIT_VM(20));
+      __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+      __builtin_amdgcn_s_barrier();
+    }
+    const int m0 = rbk(k) * WP_R;
+    const float sa = g.sa[min(m0 + (lane & 31), g.M - 1)];
+    // this wave's 4 residual rows (row 8r + wave of round r), before the next block's DMA
+    float4 rv[4][2];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long row = min(m0 + 8 * r + wave, g.M - 1);
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        rv[r][c] = *reinterpret_cast<const float4*>(g.res + row * 512 + 4 * (lane + 64 * c));
+    }
+    if (k + 1 < nblk) issue(k + 1);
+    uint8_t* const cur = lds + (k & 1) * WP_STAGE;
+    v4i acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      v4i a[2], b[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const v4i*>(cur + ((s * 2 + i) << 10) + lane * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = s < SR ? wr[s < SR ? s : 0][j]
+                      : *reinterpret_cast<const v4i*>(wl + (((wave * (8 - SR) + s - SR) * 4 + j) << 10) + lane * 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+    }
+    // y = ((acc * sa) * sw) + b; lane: rows 16i + f, columns cs + 4j + e
+    float y[2][16];
+    {
+      float sr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        sr[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sa)));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 s4 = *reinterpret_cast<const float4*>(swl + cs + 4 * j);
+        const float4 b4 = *reinterpret_cast<const float4*>(swl + 512 + cs + 4 * j);
+        const float swj[4] = {s4.x, s4.y, s4.z, s4.w}, bj[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) y[i][4 * j + e] = ((float)acc[i][j][e] * sr[i]) * swj[e] + bj[e];
+      }
+    }
+    float* const stg = reinterpret_cast<float*>(cur);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      // every wave is past its reads of the stage (the MFMAs' A, or the previous round)
+      __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+      __builtin_amdgcn_s_barrier();
+      const int i = r >> 1, h = r & 1;            // round r: rows 16i + 8h .. +7
+      if ((f >> 3) == h) {
+        const int rr = f & 7;                     // row within the round
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<float4*>(stg + rr * 512 + 4 * ((cs / 4 + j) ^ rr)) =
+              make_float4(y[i][4 * j], y[i][4 * j + 1], y[i][4 * j + 2], y[i][4 * j + 3]);
+      }
+      __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+      __builtin_amdgcn_s_barrier();
+      const int rr = wave;                        // this wave's row of the round
+      const int row = m0 + 8 * r + rr;
+      float v[1][2][4];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float4 t4 = *reinterpret_cast<const float4*>(stg + rr * 512 + 4 * ((lane + 64 * c) ^ rr));
+        v[0][c][0] = rv[r][c].x + t4.x; v[0][c][1] = rv[r][c].y + t4.y;
+        v[0][c][2] = rv[r][c].z + t4.z; v[0][c][3] = rv[r][c].w + t4.w;
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v4u{__float_as_uint(v[0][c][0]), __float_as_uint(v[0][c][1]), __float_as_uint(v[0][c][2]),
+                __float_as_uint(v[0][c][3])},
+            xrsrc, (int)(((long)row * 512 + 4 * (lane + 64 * c)) * 4), 0, 0);
+      ln_rows512<1>(v, ga, gb);
+      uint32_t qd[1][2];
+      float sc[1];
+      quant_rows512<1>(v, qd, sc);
+      __builtin_amdgcn_raw_buffer_store_b32(qd[0][0], qrsrc, (int)kp_off(row, 4 * lane, 512), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(qd[0][1], qrsrc, (int)kp_off(row, 4 * (lane + 64), 512), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc[0]), srsrc, 4 * row, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 hipError_t launch_gemm_wsx(const RowGemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return hipSuccess;
   if (g.K != WS_K || g.N != 2048 || g.epi != RE_RELU_QUANT_PMAX || g.fault.kind != FK_NONE ||
@@ -1787,6 +1965,12 @@ hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {
       g.fault.kind != FK_NONE || (g.epi == RE_RELU_QUANT_PMAX && g.pmax_n <= 0))
     return hipErrorInvalidValue;
   const int nsl = g.N / 512;
+  if (g.epi == RE_RES_LN && g.lnq && !g.lnout && !getenv_flag("QTX_WS_NOPIPE")) {
+    // k_gemm_wsr: 32-row blocks, 4+ per workgroup
+    const int nb = (g.M + WP_R - 1) / WP_R;
+    k_gemm_wsr<<<dim3(nb < 256 ? nb : 256), dim3(512), 0, st>>>(g);
+    return hipGetLastError();
+  }
   if (g.epi != RE_RES_LN && g.pmax_n <= 4 && !getenv_flag("QTX_WS_NOPIPE")) {   // pipelined
     const int nb = (g.M + WP_R - 1) / WP_R;
     int wpt = 256 / nsl;
