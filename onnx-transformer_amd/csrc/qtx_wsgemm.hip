@@ -749,6 +749,7 @@ __device__ __forceinline__ void mfma_settle(v4i (&acc)[2][4]) {
                  "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[1][2]), "+v"(acc[1][3]));
 }
 
+template <int PRIO = 0>   // PRIO: s_setprio 1 for waves 4-7 (the arbitration losers), experiment
 __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
   // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias (4 KB) | red [2][8][32] (2 KB)
@@ -764,6 +765,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   const int nb = (g.M + WP_R - 1) / WP_R;
   if (r0 >= nb) return;
   const int nblk = (nb - r0 + wpt - 1) / wpt;
+  if (PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
     const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
@@ -1501,6 +1503,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
 // iteration's stores; every iteration issues 3 stores after its DMA (dropped ones where
 // there is nothing to store) for the vmcnt(3) at the next top.
 // =====================================================================================
+template <int PRIO = 0>   // as k_gemm_wsq
 __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
   constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
   // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias (4 KB) | red [2][8][32] (2 KB)
@@ -1520,6 +1523,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
   const int t = (q >> 3) & 3, r0 = (q & 7) + 8 * (q >> 5);
   if (r0 >= nb) return;
   const int nblk = (nb - r0 + wpt - 1) / wpt;
+  if (PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
     const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
@@ -1955,6 +1959,7 @@ hipError_t launch_gemm_wsx(const RowGemmArgs& g, hipStream_t st) {
   }
   // k_gemm_wsy (MFMA-interleaved quantization) unless QTX_WSY=0 picks k_gemm_wsx
   if (const char* v = getenv("QTX_WSY"); v && *v == '0') k_gemm_wsx<<<dim3(4 * 8 * ng), dim3(512), 0, st>>>(a);
+  else if (getenv_flag("QTX_WS_PRIO")) k_gemm_wsy<1><<<dim3(4 * 8 * ng), dim3(512), 0, st>>>(a);
   else k_gemm_wsy<<<dim3(4 * 8 * ng), dim3(512), 0, st>>>(a);
   return hipGetLastError();
 }
@@ -1982,6 +1987,7 @@ hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {
         // k_gemm_wsp (0: 45.2 us) or k_gemm_wss (2: 58.7 us, experimental)
         if (const char* v = getenv("QTX_WSQ"); v && *v == '0') k_gemm_wsp<RE_QUANT><<<grid, block, 0, st>>>(g);
         else if (v && *v == '2') k_gemm_wss<<<grid, block, 0, st>>>(g);
+        else if (getenv_flag("QTX_WS_PRIO")) k_gemm_wsq<1><<<grid, block, 0, st>>>(g);
         else k_gemm_wsq<<<grid, block, 0, st>>>(g);
         break;
       case RE_RELU_PMAX:

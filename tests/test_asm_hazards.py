@@ -25,4 +25,4 @@ def test_asm_mfma_wait_states(tmp_path):
                         "k_gemm_wsq", "k_gemm_wss", "k_gemm_wsy"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-3000:]
     for k in ("k_gemm_wsq", "k_gemm_wss", "k_gemm_wsy"):
-        assert f"{k}: 0 hazards" in r.stdout
+        assert f"{k}: 0 hazards" in r.stdout, r.stdout[-2000:]

@@ -74,10 +74,14 @@ def main():
     text = open(sys.argv[1]).read().splitlines()
     total = 0
     for k in sys.argv[2:]:
-        start = next(i for i, l in enumerate(text) if re.match(rf"_ZN3qtx\d+{k}E\S*:", l))
-        end = next(i for i in range(start, len(text)) if "s_endpgm" in text[i])
-        n = check([(i + 1, text[i]) for i in range(start, end + 1)], k)
-        print(f"{k}: {n} hazards")
+        # every instance (template kernels: one per instantiation)
+        starts = [i for i, l in enumerate(text) if re.match(rf"_ZN3qtx\d+{k}[EI]\S*:", l)]
+        assert starts, f"kernel {k} not found"
+        n = 0
+        for start in starts:
+            end = next(i for i in range(start, len(text)) if "s_endpgm" in text[i])
+            n += check([(i + 1, text[i]) for i in range(start, end + 1)], text[start].rstrip(":"))
+        print(f"{k}: {n} hazards ({len(starts)} instances)")
         total += n
     sys.exit(1 if total else 0)
 
