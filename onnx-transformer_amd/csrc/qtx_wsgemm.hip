@@ -1970,8 +1970,12 @@ hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {
       g.fault.kind != FK_NONE || (g.epi == RE_RELU_QUANT_PMAX && g.pmax_n <= 0))
     return hipErrorInvalidValue;
   const int nsl = g.N / 512;
-  if (g.epi == RE_RES_LN && g.lnq && !g.lnout && !getenv_flag("QTX_WS_NOPIPE")) {
-    // k_gemm_wsr: 32-row blocks, 4+ per workgroup
+  const char* wsr = getenv("QTX_WSR");
+  if (g.epi == RE_RES_LN && g.lnq && !g.lnout && !getenv_flag("QTX_WS_NOPIPE") &&
+      !(wsr && *wsr == '0')) {
+    // k_gemm_wsr (QTX_WSR=0: k_gemm_ws<RE_RES_LN>): the decode's encoder at B = 32 (M = 2304)
+    // 0.656 -> 0.616 ms; at cfg3's M = 32768 the KP row GEMM stays faster (40.3 vs 43.5 us,
+    // qtx_api.hip ws_res_ok)
     const int nb = (g.M + WP_R - 1) / WP_R;
     k_gemm_wsr<<<dim3(nb < 256 ? nb : 256), dim3(512), 0, st>>>(g);
     return hipGetLastError();
