@@ -749,14 +749,19 @@ __device__ __forceinline__ void mfma_settle(v4i (&acc)[2][4]) {
                  "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[1][2]), "+v"(acc[1][3]));
 }
 
-template <int PRIO = 0>   // PRIO: s_setprio 1 for waves 4-7 (the arbitration losers), experiment
+// PRIO: s_setprio 1 for waves 4-7 (the arbitration losers), experiment.  LAG: a pinned MFMA
+// waits for the quantized output LAG places back (1: the one just before it), so the
+// quantization's dependent VALU chain need not finish before the next MFMA issues; 2 and 3
+// measured no faster (QKV 40.5 / 40.4 vs 40.0 us, FFN1 70.9 / 70.0 vs 68.1 us).
+template <int PRIO = 0, int LAG = 1>
 __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
   // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias (4 KB) | red [2][8][32] (2 KB)
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4 + 2 * 8 * 64 * 4];
   uint8_t* const wl = lds + 2 * WP_STAGE;
   float* const swl = reinterpret_cast<float*>(wl + WL);
   float* const red0 = swl + 1024;                            // [2][8][32]
+  float* const sal = red0 + 2 * 8 * WP_R;                    // [2][8 waves][64]: row scales
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int f = lane & 15, gq = lane >> 4;
   const int nsl = g.N >> 9;
@@ -775,6 +780,16 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
                  : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
   };
   auto rbk = [&](int k) { return r0 + min(k, nblk - 1) * wpt; };
+  // block k's A rows and, per wave, its 32 row scales (lanes 32-63 repeat them) by LDS-DMA:
+  // no global load in the loop whose wait the compiler would count past the DMA (its
+  // counted vmcnt does not see the asm DMAs, so it would also wait for them)
+  auto dma4 = [](const float* gsrc, const float* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
   auto issue = [&](int k) {
     uint8_t* st = lds + (k & 1) * WP_STAGE;
 #pragma unroll
@@ -782,6 +797,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
       const long row = min(rbk(k) * WP_R + 16 * i + f, g.M - 1);
       dma16(g.A + kp_off(row, 64 * wave + 16 * gq, WS_K), st + ((wave * 2 + i) << 10));
     }
+    dma4(g.sa + min(rbk(k) * WP_R + (lane & 31), g.M - 1), sal + ((k & 1) * 8 + wave) * 64);
   };
   issue(0);
   v4i wr[SR][4];
@@ -809,7 +825,6 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   const __amdgpu_buffer_rsrc_t orsrc = ws_rsrc(g.out8 + (long)t * g.o8_ts, (long)g.M * g.ldo8);
   const __amdgpu_buffer_rsrc_t srsrc = ws_rsrc(g.os + (long)t * g.os_ts, 4L * g.M);
   auto redb = [&](int k) { return red0 + (k & 1) * 8 * WP_R; };
-  auto sa_of = [&](int k) { return g.sa[min(rbk(k) * WP_R + (lane & 31), g.M - 1)]; };
   auto top_wait = [&]() {
     // the block's DMA retired (behind it only the previous iteration's 3 stores per wave)
     __builtin_amdgcn_s_waitcnt(WAIT_VM(3));
@@ -817,11 +832,10 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
     __builtin_amdgcn_s_barrier();
   };
   // y of block k (acc, row scale sa) and the wave's partial row maxima into red[k & 1]
-  auto form_y = [&](v4i (&acc)[2][4], float sa, float (&y)[2][16], int k) {
+  auto form_y = [&](v4i (&acc)[2][4], float (&y)[2][16], int k) {
     float sr[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      sr[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sa)));
+    for (int i = 0; i < 2; ++i) sr[i] = sal[((k & 1) * 8 + wave) * 64 + 16 * i + f];
     float am[2] = {0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -869,7 +883,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   auto mfma_block = [&](v4i (&acc)[2][4], const uint8_t* cur, bool q, int kq, float (&y)[2][16]) {
     float bq[2] = {0.0f, 0.0f}, iq[2] = {0.0f, 0.0f};
     if (q) scales(kq, bq, iq);
-    float last = 0.0f, tq[4];
+    float hist[3] = {0.0f, 0.0f, 0.0f}, tq[4];   // results of the last outputs, newest first
     uint32_t d[4];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -892,10 +906,10 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
             // quantized output o of block k-1: row fragment ii, column group jj, element e
             const int o = n >> 1, ii = o >> 4, jj = (o >> 2) & 3, e = o & 3;
             float yv = y[ii][4 * jj + e];
-            if (s == 0) mfma_pin<true>(acc[i][j], b[j], a[i], last, yv);
-            else mfma_pin<false>(acc[i][j], b[j], a[i], last, yv);
+            if (s == 0) mfma_pin<true>(acc[i][j], b[j], a[i], hist[LAG - 1], yv);
+            else mfma_pin<false>(acc[i][j], b[j], a[i], hist[LAG - 1], yv);
             tq[e] = rint_biased(div_cr(yv, bq[ii], iq[ii]));
-            last = tq[e];
+            hist[2] = hist[1]; hist[1] = hist[0]; hist[0] = tq[e];
             if (e == 3) {
               d[jj] = pack4_biased(tq[0], tq[1], tq[2], tq[3]);
               if (jj == 3) store_row(kq, ii, d);
@@ -919,21 +933,19 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
   __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
   __builtin_amdgcn_s_barrier();
-  float sa = sa_of(0);
   issue(1);
   mfma_block(acc, lds, false, 0, y);
-  form_y(acc, sa, y, 0);
+  form_y(acc, y, 0);
   const long long st_1 = QTX_NOW();
   // ---- block k: MFMAs with the quantization of block k-1, then the y of block k
   for (int k = 1; k < nblk; ++k) {
     const long long t0 = QTX_NOW();
     top_wait();
     const long long t1 = QTX_NOW();
-    sa = sa_of(k);
     issue(k + 1);
     mfma_block(acc, lds + (k & 1) * WP_STAGE, true, k - 1, y);
     const long long t2 = QTX_NOW();
-    form_y(acc, sa, y, k);
+    form_y(acc, y, k);
     const long long t3 = QTX_NOW();
     st_top += t1 - t0;
     st_mm += t2 - t1;
@@ -991,13 +1003,15 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
 // a block's accumulators across one barrier; each wave holds one y buffer.
 // =====================================================================================
 __global__ __launch_bounds__(512) void k_gemm_wss(RowGemmArgs g) {
+  constexpr int LAG = 1;
   constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
   // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias (4 KB) | red [2][8][32] (2 KB)
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4 + 2 * 8 * 64 * 4];
   __shared__ unsigned ydone;                                 // B waves' finished Y phases
   uint8_t* const wl = lds + 2 * WP_STAGE;
   float* const swl = reinterpret_cast<float*>(wl + WL);
   float* const red0 = swl + 1024;                            // [2][8][32]
+  float* const sal = red0 + 2 * 8 * WP_R;                    // [2][8 waves][64]: row scales
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int f = lane & 15, gq = lane >> 4;
   const bool grpB = __builtin_amdgcn_readfirstlane(wave) >= 4;
@@ -1017,13 +1031,21 @@ __global__ __launch_bounds__(512) void k_gemm_wss(RowGemmArgs g) {
                  : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
   };
   auto rbk = [&](int k) { return r0 + min(k, nblk - 1) * wpt; };
-  auto issue = [&](int k) {
+  auto dma4 = [](const float* gsrc, const float* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto issue = [&](int k) {      // block k's A rows and its row scales (as k_gemm_wsq)
     uint8_t* st = lds + (k & 1) * WP_STAGE;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const long row = min(rbk(k) * WP_R + 16 * i + f, g.M - 1);
       dma16(g.A + kp_off(row, 64 * wave + 16 * gq, WS_K), st + ((wave * 2 + i) << 10));
     }
+    dma4(g.sa + min(rbk(k) * WP_R + (lane & 31), g.M - 1), sal + ((k & 1) * 8 + wave) * 64);
   };
   issue(0);
   v4i wr[SR][4];
@@ -1051,7 +1073,10 @@ __global__ __launch_bounds__(512) void k_gemm_wss(RowGemmArgs g) {
   const __amdgpu_buffer_rsrc_t orsrc = ws_rsrc(g.out8 + (long)t * g.o8_ts, (long)g.M * g.ldo8);
   const __amdgpu_buffer_rsrc_t srsrc = ws_rsrc(g.os + (long)t * g.os_ts, 4L * g.M);
   auto redb = [&](int k) { return red0 + (k & 1) * 8 * WP_R; };
-  auto sa_of = [&](int k) { return g.sa[min(rbk(k) * WP_R + (lane & 31), g.M - 1)]; };
+  auto sr_of = [&](int k, float (&sr)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) sr[i] = sal[((k & 1) * 8 + wave) * 64 + 16 * i + f];
+  };
   auto top_wait = [&]() {
     __builtin_amdgcn_s_waitcnt(WAIT_VM(3));      // behind the block's DMA: 3 stores per wave
     __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
@@ -1073,11 +1098,10 @@ __global__ __launch_bounds__(512) void k_gemm_wss(RowGemmArgs g) {
     }
   };
   // Y: y of block k from acc (row scale sa) and the wave's partial row maxima -> red[k & 1]
-  auto form_y = [&](v4i (&acc)[2][4], float sa, float (&y)[2][16], int k) {
-    float sr[2];
+  auto form_y = [&](v4i (&acc)[2][4], const float (&sr_in)[2], float (&y)[2][16], int k) {
+    float sr[2];     // B: read at the top of its iteration, before the DMA reuses the stage
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      sr[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sa)));
+    for (int i = 0; i < 2; ++i) sr[i] = sr_in[i];
     float am[2] = {0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1140,7 +1164,7 @@ __global__ __launch_bounds__(512) void k_gemm_wss(RowGemmArgs g) {
     const uint8_t* cur = lds + (k & 1) * WP_STAGE;
     float bq[2] = {0.0f, 0.0f}, iq[2] = {0.0f, 0.0f};
     if constexpr (Q) scales(kq, bq, iq);
-    float last = 0.0f, tq[4];
+    float hist[3] = {0.0f, 0.0f, 0.0f}, tq[4];   // results of the last outputs, newest first
     uint32_t d[4];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -1162,10 +1186,10 @@ __global__ __launch_bounds__(512) void k_gemm_wss(RowGemmArgs g) {
           } else {
             const int o = n >> 1, ii = o >> 4, jj = (o >> 2) & 3, e = o & 3;
             float yv = y[ii][4 * jj + e];
-            if (s == 0) mfma_pin<true>(acc[i][j], b[j], a[i], last, yv);
-            else mfma_pin<false>(acc[i][j], b[j], a[i], last, yv);
+            if (s == 0) mfma_pin<true>(acc[i][j], b[j], a[i], hist[LAG - 1], yv);
+            else mfma_pin<false>(acc[i][j], b[j], a[i], hist[LAG - 1], yv);
             tq[e] = rint_biased(div_cr(yv, bq[ii], iq[ii]));
-            last = tq[e];
+            hist[2] = hist[1]; hist[1] = hist[0]; hist[0] = tq[e];
             if (e == 3) {
               d[jj] = pack4_biased(tq[0], tq[1], tq[2], tq[3]);
               if (jj == 3) store_row(kq, ii, d);
@@ -1178,19 +1202,18 @@ __global__ __launch_bounds__(512) void k_gemm_wss(RowGemmArgs g) {
   const std::true_type T_{};
   const std::false_type F_{};
 
-  v4i acc[2][4];
-  float y[2][16];
   __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
   __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
   __builtin_amdgcn_s_barrier();
-  float san = sa_of(0);                    // the row scales of this wave's next Y
-  for (int k = 0; k <= nblk; ++k) {
-    if (k > 0) top_wait();
-    const float sac = san;
-    if (!grpB) san = sa_of(k + 1);
-    else if (k < nblk) san = sa_of(k);
-    if (k + 1 < nblk) issue(k + 1);
-    if (!grpB) {
+  // one loop per group (the same iterations and barriers): a loop shared by both would carry
+  // the union of their loop-carried values (A: y, B: acc) and spill — and a spill reload's
+  // wait is vmcnt(0), which also waits for the next block's DMA and every store
+  if (!grpB) {
+    v4i acc[2][4];
+    float y[2][16];
+    for (int k = 0; k <= nblk; ++k) {
+      if (k > 0) top_wait();
+      if (k + 1 < nblk) issue(k + 1);
       if (k < nblk) mfma_block(acc, k, F_, 0, y);
       if (k >= 1) {
         wait_y(k);                          // B's partial maxima of block k-1
@@ -1198,10 +1221,25 @@ __global__ __launch_bounds__(512) void k_gemm_wss(RowGemmArgs g) {
       } else {
         dummy_stores();
       }
-      if (k < nblk) form_y(acc, sac, y, k);
-    } else {
+      if (k < nblk) {
+        float sr[2];
+        sr_of(k, sr);
+        form_y(acc, sr, y, k);
+      }
+    }
+  } else {
+    v4i acc[2][4];
+    float y[2][16];
+    for (int k = 0; k <= nblk; ++k) {
+      if (k > 0) top_wait();
+      float sr[2];
+      if (k >= 1) {                         // block k-1's scales, before DMA(k+1) reuses the stage
+        sr_of(k - 1, sr);
+        __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+      }
+      if (k + 1 < nblk) issue(k + 1);
       if (k >= 1) {
-        form_y(acc, sac, y, k - 1);
+        form_y(acc, sr, y, k - 1);
         if (lane == 0) __hip_atomic_fetch_add(&ydone, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         wait_y(k);                          // every B wave's partials of block k-1
       }
@@ -1503,14 +1541,15 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
 // iteration's stores; every iteration issues 3 stores after its DMA (dropped ones where
 // there is nothing to store) for the vmcnt(3) at the next top.
 // =====================================================================================
-template <int PRIO = 0>   // as k_gemm_wsq
+template <int PRIO = 0, int LAG = 1>   // as k_gemm_wsq
 __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
   constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
   // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias (4 KB) | red [2][8][32] (2 KB)
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4 + 2 * 8 * 64 * 4];
   uint8_t* const wl = lds + 2 * WP_STAGE;
   float* const swl = reinterpret_cast<float*>(wl + WL);
   float* const red0 = swl + 1024;                            // [2][8][32]
+  float* const sal = red0 + 2 * 8 * WP_R;                    // [2][8 waves][64]: row scales
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int f = lane & 15, gq = lane >> 4;
   const int nb = (g.M + WP_R - 1) / WP_R;
@@ -1533,13 +1572,21 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
                  : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
   };
   auto rbk = [&](int k) { return r0 + min(k, nblk - 1) * wpt; };
-  auto issue = [&](int k) {
+  auto dma4 = [](const float* gsrc, const float* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto issue = [&](int k) {      // block k's A rows and its row scales (as k_gemm_wsq)
     uint8_t* st = lds + (k & 1) * WP_STAGE;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const long row = min(rbk(k) * WP_R + 16 * i + f, g.M - 1);
       dma16(g.A + kp_off(row, 64 * wave + 16 * gq, WS_K), st + ((wave * 2 + i) << 10));
     }
+    dma4(g.sa + min(rbk(k) * WP_R + (lane & 31), g.M - 1), sal + ((k & 1) * 8 + wave) * 64);
   };
   issue(0);
   v4i wr[SR][4];
@@ -1568,18 +1615,16 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
   const __amdgpu_buffer_rsrc_t orsrc = ws_rsrc(g.out8, (long)(g.M + (g.M & 1)) * g.ldo8);
   const __amdgpu_buffer_rsrc_t srsrc = ws_rsrc(g.os, t == 0 ? 4L * g.M : 0L);
   auto redb = [&](int k) { return red0 + (k & 1) * 8 * WP_R; };
-  auto sa_of = [&](int k) { return g.sa[min(rbk(k) * WP_R + (lane & 31), g.M - 1)]; };
   auto dummy_stores = [&]() {
     const __amdgpu_buffer_rsrc_t nul = ws_rsrc(g.out8, 0L);
 #pragma unroll
     for (int d2 = 0; d2 < 3; ++d2) __builtin_amdgcn_raw_buffer_store_b32(0u, nul, 0, 0, 0);
   };
   // Y: y of block k (ReLU) from acc and the wave's partial row maxima -> red[k & 1]
-  auto form_y = [&](v4i (&acc)[2][4], float sa, float (&y)[2][16], int k) {
+  auto form_y = [&](v4i (&acc)[2][4], float (&y)[2][16], int k) {
     float sr[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      sr[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sa)));
+    for (int i = 0; i < 2; ++i) sr[i] = sal[((k & 1) * 8 + wave) * 64 + 16 * i + f];
     float am[2] = {0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1678,7 +1723,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
     const uint8_t* cur = lds + (k & 1) * WP_STAGE;
     float bq[2] = {0.0f, 0.0f}, iq[2] = {0.0f, 0.0f};
     if constexpr (Q) scales(kq, m, bq, iq);
-    float last = 0.0f, tq[4];
+    float hist[3] = {0.0f, 0.0f, 0.0f}, tq[4];   // results of the last outputs, newest first
     uint32_t d[4];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -1700,10 +1745,10 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
           } else {
             const int o = n >> 1, ii = o >> 4, jj = (o >> 2) & 3, e = o & 3;
             float yv = y[ii][4 * jj + e];
-            if (s == 0) mfma_pin<true>(acc[i][j], b[j], a[i], last, yv);
-            else mfma_pin<false>(acc[i][j], b[j], a[i], last, yv);
+            if (s == 0) mfma_pin<true>(acc[i][j], b[j], a[i], hist[LAG - 1], yv);
+            else mfma_pin<false>(acc[i][j], b[j], a[i], hist[LAG - 1], yv);
             tq[e] = rint_biased(div_cr(yv, bq[ii], iq[ii]));
-            last = tq[e];
+            hist[2] = hist[1]; hist[1] = hist[0]; hist[0] = tq[e];
             if (e == 3) {
               d[jj] = pack4_biased(tq[0], tq[1], tq[2], tq[3]);
               if (jj == 3) store_row(kq, ii, d);
@@ -1733,7 +1778,6 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
     }
     float m2 = 0.0f;
     if (k >= 2) m2 = full_max(k - 2, mb);       // granule loads: before this iteration's DMA
-    const float sa = sa_of(k);
     if (k >= 1 && k <= nblk) {
       mo = slice_max(k - 1);
       publish(k - 1, mo);
@@ -1742,7 +1786,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
     if (k < nblk) {
       if (k >= 2) mfma_block(acc, k, T_, k - 2, yb, m2);
       else mfma_block(acc, k, F_, 0, yb, 0.0f);
-      form_y(acc, sa, yb, k);
+      form_y(acc, yb, k);
     } else if (k >= 2) {
       quant_all(k - 2, yb, m2);
     } else {
