@@ -753,7 +753,10 @@ __device__ __forceinline__ void mfma_settle(v4i (&acc)[2][4]) {
 // waits for the quantized output LAG places back (1: the one just before it), so the
 // quantization's dependent VALU chain need not finish before the next MFMA issues; 2 and 3
 // measured no faster (QKV 40.5 / 40.4 vs 40.0 us, FFN1 70.9 / 70.0 vs 68.1 us).
-template <int PRIO = 0, int LAG = 1>
+// XG: the nsl column-slice workgroups of a row group on one XCD (blockIdx % 8 under
+// round-robin placement — speed only), dispatched together, so a row block's A is fetched
+// from HBM once and read from L2 by the other slices (0: slice = blockIdx % nsl)
+template <int PRIO = 0, int LAG = 1, int XG = 1>
 __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
   // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias (4 KB) | red [2][8][32] (2 KB)
@@ -766,7 +769,20 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   const int f = lane & 15, gq = lane >> 4;
   const int nsl = g.N >> 9;
   const int wpt = gridDim.x / nsl;
-  const int t = blockIdx.x % nsl, r0 = blockIdx.x / nsl;
+  int t = blockIdx.x % nsl, r0 = blockIdx.x / nsl;
+  if (XG) {
+    // the first 8 * nsl * A workgroups: XCD x, slot j -> slice j % nsl of row group
+    // 8 * (j / nsl) + x; the rest (fewer than 8 * nsl) in blockIdx order after them
+    const int b = blockIdx.x, A = gridDim.x / (8 * nsl), aligned = 8 * nsl * A;
+    if (b < aligned) {
+      const int j = b >> 3;
+      t = j % nsl;
+      r0 = 8 * (j / nsl) + (b & 7);
+    } else {
+      t = (b - aligned) % nsl;
+      r0 = 8 * A + (b - aligned) / nsl;
+    }
+  }
   const int nb = (g.M + WP_R - 1) / WP_R;
   if (r0 >= nb) return;
   const int nblk = (nb - r0 + wpt - 1) / wpt;
@@ -2036,6 +2052,7 @@ hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {
         if (const char* v = getenv("QTX_WSQ"); v && *v == '0') k_gemm_wsp<RE_QUANT><<<grid, block, 0, st>>>(g);
         else if (v && *v == '2') k_gemm_wss<<<grid, block, 0, st>>>(g);
         else if (getenv_flag("QTX_WS_PRIO")) k_gemm_wsq<1><<<grid, block, 0, st>>>(g);
+        else if (const char* x = getenv("QTX_WS_XG"); x && *x == '0') k_gemm_wsq<0, 1, 0><<<grid, block, 0, st>>>(g);
         else k_gemm_wsq<<<grid, block, 0, st>>>(g);
         break;
       case RE_RELU_PMAX:
