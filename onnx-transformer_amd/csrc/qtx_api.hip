@@ -64,6 +64,12 @@ struct QLin {
   int N = 0, K = 0;
   int8_t* qkp = nullptr;   // encoder, 8-bit: q in the row GEMM's KP layout (pack_w_kp)
   int8_t* qws = nullptr;   // encoder, 8-bit, K == 512: q in the weight-stationary order
+  // 4-bit models: the int4 values (in [-7, 7]) unpacked to int8 [N, K] once at load, so the
+  // int8 kernels run them — exact (integer products), and the decode is latency-bound, so
+  // the packed form's half bytes bought nothing while its unpack lengthened every kernel
+  // (cfg4 15.97 vs cfg2 14.45 ms per decode at r03d).  q stays packed (qtx_model_linear).
+  int8_t* q8 = nullptr;
+  const int8_t* w8() const { return q8 ? q8 : q; }   // the int8 form (8-bit models: q)
 };
 
 struct EncLayer {
@@ -212,6 +218,8 @@ int quantize_into(const qtx_config& c, QLin& L, int row0, const float* W, const 
     HIPCHK(launch_rows(a, st));
     HIPCHK(launch_pack_int4(tmp, N, K, reinterpret_cast<uint8_t*>(L.q) + (size_t)row0 * K / 2,
                             st));
+    if (L.q8)
+      HIPCHK(hipMemcpyAsync(L.q8 + (size_t)row0 * K, tmp, (size_t)N * K, hipMemcpyDeviceToDevice, st));
   }
   HIPCHK(hipMemcpyAsync(L.b + row0, b, N * sizeof(float), hipMemcpyDeviceToDevice, st));
   return QTX_OK;
@@ -248,16 +256,16 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     auto lin = [&](QLin& L, int N, int K) {
       L.N = N; L.K = K;
       L.q = ar.take<int8_t>(wbytes(c, N, K));
+      if (c.weight_bits == 4) L.q8 = ar.take<int8_t>((size_t)N * K);
       L.s = ar.take<float>(N);
       L.b = ar.take<float>(N);
     };
     m->enc.resize(NL);
     m->dec.resize(NL);
     for (auto& e : m->enc) { lin(e.qkv, 3 * D, D); lin(e.o, D, D); lin(e.w1, F, D); lin(e.w2, D, F); }
-    if (c.weight_bits == 8)      // KP copies for the encoder's row GEMMs
-      for (auto& e : m->enc)
+    for (auto& e : m->enc)
         for (QLin* L : {&e.qkv, &e.o, &e.w1, &e.w2}) L->qkp = ar.take<int8_t>((size_t)L->N * L->K);
-    if (c.weight_bits == 8 && c.d_ff % 512 == 0)   // weight-stationary copies (K = 512 GEMMs)
+    if (c.d_ff % 512 == 0)   // weight-stationary copies (K = 512 GEMMs)
       for (auto& e : m->enc)
         for (QLin* L : {&e.qkv, &e.o, &e.w1}) L->qws = ar.take<int8_t>((size_t)L->N * L->K);
     for (auto& d : m->dec) {
@@ -323,8 +331,8 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
   if (rc) { qtx_model_destroy(m); return rc; }
   for (auto& e : m->enc)
     for (QLin* L : {&e.qkv, &e.o, &e.w1, &e.w2})
-      if ((L->qkp && launch_pack_w_kp(L->q, L->N, L->K, L->qkp, st) != hipSuccess) ||
-          (L->qws && launch_pack_w_ws(L->q, L->N, L->K, L->qws, st) != hipSuccess)) {
+      if ((L->qkp && launch_pack_w_kp(L->w8(), L->N, L->K, L->qkp, st) != hipSuccess) ||
+          (L->qws && launch_pack_w_ws(L->w8(), L->N, L->K, L->qws, st) != hipSuccess)) {
         qtx_model_destroy(m);
         return fail(QTX_E_HIP, "KP / WS weight pack");
       }
@@ -532,16 +540,17 @@ int linear(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa
            int flags, const float* res, float* out, long ldo, hipStream_t st) {
   GemmArgs g{};
   g.A = a8; g.lda = L.K; g.sa = sa;
-  g.W = L.q; g.ldw = c.weight_bits == 8 ? L.K : L.K / 2; g.sw = L.s; g.bias = L.b;
+  const int wb = L.q8 ? 8 : c.weight_bits;
+  g.W = L.w8(); g.ldw = wb == 8 ? L.K : L.K / 2; g.sw = L.s; g.bias = L.b;
   g.out = out; g.ldo = ldo; g.res = res; g.ldr = ldo;
   g.M = M; g.N = L.N; g.K = L.K; g.flags = flags;
-  HIPCHK(launch_gemm(g, c.weight_bits, st));
+  HIPCHK(launch_gemm(g, wb, st));
   return QTX_OK;
 }
 
 // Row-complete GEMM (k_gemm_row) for 8-bit weights: epilogues of whole 512-wide rows.
-bool row_path(const qtx_config& c) {
-  return c.weight_bits == 8 && c.d_ff % 512 == 0 && !getenv("QTX_NO_ROWGEMM");
+bool row_path(const qtx_config& c) {   // (4-bit models: on the unpacked int8 weights)
+  return c.d_ff % 512 == 0 && !getenv("QTX_NO_ROWGEMM");
 }
 // kp: A (a8) in the KP layout and W from L.qkp; the int8 lnq / FFN-hidden outputs are
 // then written KP as well (RE_QUANT's q8 stays row-major: attention reads it).
@@ -570,7 +579,7 @@ RowGemmArgs rowgemm(const QLin& L, const int8_t* a8, const float* sa, int M, int
   RowGemmArgs g{};
   const bool ws = kp && L.qws && L.K == 512 &&
                   (epi == RE_RES_LN ? ws_res_ok(M) : M >= ws_min_m());
-  g.A = a8; g.lda = L.K; g.sa = sa; g.W = ws ? L.qws : kp ? L.qkp : L.q; g.ldw = L.K;
+  g.A = a8; g.lda = L.K; g.sa = sa; g.W = ws ? L.qws : kp ? L.qkp : L.w8(); g.ldw = L.K;
   g.sw = L.s; g.bias = L.b;
   g.M = M; g.N = L.N; g.K = L.K; g.epi = epi; g.kp = ws ? 2 : kp;
   return g;
@@ -773,7 +782,8 @@ int check_fault(const qtx_model* m, const qtx_fault* f, int module, long B, long
   if (!f || f->kind == QTX_FAULT_NONE) return QTX_OK;
   const qtx_config& c = m->cfg;
   const long M = B * Sq, Ms = B * Ss;
-  if (!row_path(c)) return fail(QTX_E_UNSUPPORTED, "fault injection needs 8-bit weights");
+  if (!row_path(c) || c.weight_bits != 8)
+    return fail(QTX_E_UNSUPPORTED, "fault injection needs 8-bit weights");
   if (f->kind < 0 || f->kind > QTX_FAULT_OUTPUT) return fail(QTX_E_INVALID, "fault kind %d", f->kind);
   if (f->module != module) return fail(QTX_E_INVALID, "fault module %d", f->module);
   if (f->layer < 0 || f->layer >= c.n_layers) return fail(QTX_E_INVALID, "fault layer %d", f->layer);
@@ -1061,7 +1071,9 @@ bool env_flag(const char* name);
 // ---- fused decode step (M = B rows, keys <= 128) ----------------------------------------
 SkinnyArgs skinny(int wbits, const QLin& L, int M, int amode, int flags, float* out, long ldo) {
   SkinnyArgs s{};
-  s.amode = amode; s.W = L.q; s.ldw = wbits == 8 ? L.K : L.K / 2; s.sw = L.s; s.bias = L.b;
+  // wbits 8 on a 4-bit model: its unpacked int8 copy
+  s.amode = amode; s.W = wbits == 8 ? L.w8() : L.q; s.ldw = wbits == 8 ? L.K : L.K / 2;
+  s.sw = L.s; s.bias = L.b;
   s.out = out; s.ldo = ldo; s.M = M; s.N = L.N; s.K = L.K; s.flags = flags;
   return s;
 }
@@ -1073,7 +1085,7 @@ SkinnyArgs skinny(int wbits, const QLin& L, int M, int amode, int flags, float* 
 int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len,
                       int64_t* ids, const uint8_t* src_mask, hipStream_t st) {
   const qtx_config& c = m->cfg;
-  const int D = c.d_model, F = c.d_ff, wb = c.weight_bits;
+  const int D = c.d_model, F = c.d_ff, wb = m->dec[0].qkv.q8 ? 8 : c.weight_bits;
   const bool ffn_qkernel = env_flag("QTX_FFN_QKERNEL");
   const bool fused_ln = !env_flag("QTX_SPLIT_LN");
   Scratch& s = g.dec;
