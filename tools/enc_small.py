@@ -11,7 +11,8 @@ from qtx.model import QtxModel  # noqa: E402
 from qtx.weights import ModelConfig, synthetic_state_dict  # noqa: E402
 
 m = QtxModel(synthetic_state_dict(20241223), ModelConfig())
-for B, S in [(32, 72), (256, 72)]:
+cfgs = [(int(b), 72) for b in sys.argv[1:]] or [(32, 72), (256, 72)]
+for B, S in cfgs:
     x = torch.randn((B, S, 512), device="cuda")
     mk = torch.ones((B, S), dtype=torch.uint8, device="cuda")
     for _ in range(3):
