@@ -279,6 +279,12 @@ typedef struct qtx_row_gemm {
    * invalid).  NULL: the flag is the u32 at byte offset 1024 * ceil(M / 32) + 4 of pmax_out,
    * zeroed by each launch; read it after the stream completes. */
   uint32_t* status;
+  /* epi 1 with kp = 1 only: split K over `ksplit` workgroups per 128-row tile (ksplit in
+   * {2, 4, 8}, (K / 64) % (4 * ksplit) == 0), int32 partials in `part` (>= ksplit * M * 2 KB
+   * of device scratch), then a row-wise residual + LayerNorm + quant epilogue; the same
+   * results.  What the encoder does for FFN2 below 64 row tiles.  0: no split. */
+  int32_t* part;
+  int32_t ksplit;
 } qtx_row_gemm;
 int32_t qtx_linear_rows(const qtx_row_gemm* args, void* stream);
 /* W int8 [N, K] row-major -> out [N, K] in the KP layout with the per-512-column-tile row

@@ -584,7 +584,8 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   const float q_own = yr[h * 64 + lane];
   const float k_own = KV_NEW ? yr[512 + h * 64 + lane] : 0.0f;
   const float v_own = KV_NEW ? yr[1024 + h * 64 + lane] : 0.0f;
-  const int step = KV_NEW ? *a.step : 0;
+  // clamped: a stale position (a counter not reset) must not index past the cache
+  const int step = KV_NEW ? min(max(*a.step, 0), (int)a.kv_bs - 1) : 0;
   const int rsub = lane >> 2, ch = lane & 3;
   uint4 kr[NIT], vr[NIT];
 #pragma unroll
@@ -994,7 +995,7 @@ __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int 
     id = wave_min_i32(lane < 16 && gv == gb ? redi[lane] : 0x7fffffff);
     id = min(id, V - 1);                   // keeps the embedding gather in bounds, whatever
   }
-  if (tid == 0) ids[m * ids_bs + s + 1] = id;
+  if (tid == 0 && s >= 0 && s + 1 < ids_bs) ids[m * ids_bs + s + 1] = id;   // bounded (stale position)
   QTX_STAMP(4);
   // next decoder input: tgt_embed(id) at position s + 1 (embeddings.py:12-13)
   if (tid < 128) {

@@ -263,7 +263,9 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
     // 64 B with the conflict-free slot swizzle of k_gemm256 (g_slot).  Wave w moves A row
     // pairs 8w..8w+7 (1 piece) and W row pairs 32w..32w+31 (4 pieces) per step.
     constexpr int KB = 64, KA = R_BM * KB, KSTG = (R_BM + R_BN) * KB;   // 8 KB, 40 KB
-    const int nk = g.K / KB;                      // multiple of 4 (launch check)
+    // split K (RE_PARTIAL): this workgroup's K range is chunks [kb0, kb0 + nk)
+    const int nk = g.K / KB / (int)gridDim.y;     // multiple of 4 (launch check)
+    const int kb0 = (int)blockIdx.y * nk;
     const long lpr = g.K >> 6;                    // 128-byte lines per row pair
     const int q = lane & 7, pr = lane >> 3;       // line chunk, pair within the piece
     const int rsub = 2 * pr + (q >> 2), slot = q & 3;   // LDS row within the piece, slot
@@ -284,7 +286,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
       // exactly 5 DMAs and the vmcnt counts stay constant
       int kk = min(kt, nk - 1) + krot;
       if (kk >= nk) kk -= nk;
-      const long k0 = (long)kk << 7;              // line index offset of K chunk kk
+      const long k0 = (long)(kk + kb0) << 7;      // line index offset of K chunk kk
 #ifdef QTX_DIAG_NODMA                             // diagnostic builds only (bound decomposition)
       return;
 #endif
@@ -327,7 +329,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
       __builtin_amdgcn_s_barrier();
       int kk = min(kt + 3, nk - 1) + krot;
       if (kk >= nk) kk -= nk;
-      const long k0 = (long)kk << 7;
+      const long k0 = (long)(kk + kb0) << 7;
       const uint8_t* Bs = cur + KA;
       v4i bfr[8];
 #pragma unroll
@@ -437,6 +439,23 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
   }
   __syncthreads();                                 // all fragment reads done: LDS reusable
   QTX_STAMP(1);
+  if constexpr (EPI == RE_PARTIAL) {
+    // the raw accumulators of this K range: lane rows 4 fg + e of fragment i, 8 consecutive
+    // columns n0 + wn * 128 + 8 fr .. + 7 (two 16-byte stores; 16 lanes = 512 B of a row)
+    int32_t* dst = g.part + (long)blockIdx.y * g.M * 512;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long row = m0 + wm * 64 + i * 16 + 4 * fg + e;
+        if (FULL || row < g.M) {
+          int4* d = reinterpret_cast<int4*>(dst + row * 512 + n0 + wn * 128 + 8 * fr);
+          d[0] = make_int4(acc[i][0][e], acc[i][1][e], acc[i][2][e], acc[i][3][e]);
+          d[1] = make_int4(acc[i][4][e], acc[i][5][e], acc[i][6][e], acc[i][7][e]);
+        }
+      }
+    return;
+  } else {
   if (FAULT && (g.fault.kind == FK_INPUT || g.fault.kind == FK_WEIGHT)) {
     // exact integer correction of the accumulators for one bit-flipped int8 operand
     // (the perturbation the reference propagates through the MatMul, inject_utils/layers.py)
@@ -721,6 +740,59 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
     }
     QTX_STAMP(2);
   }
+  }  // EPI != RE_PARTIAL
+}
+
+// The split-K RE_RES_LN epilogue: one wave per row — the ksplit int32 partials summed
+// (exact), y = ((float(acc) * sa) * sw) + b, x = res + y (stored), then LayerNorm and the
+// per-token quantization (KP out) or the fp32 LayerNorm output: the same arithmetic, in
+// the same order, as k_gemm_row<RE_RES_LN>'s epilogue.
+__global__ __launch_bounds__(256) void k_res_ln_partials(RowGemmArgs g) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + wave;
+  if (row >= g.M) return;                          // whole wave: no barrier below
+  int4 p[2];
+  float4 r4[2], s4[2], b4[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    p[c] = make_int4(0, 0, 0, 0);
+    for (int z = 0; z < g.ksplit; ++z) {
+      const int4 t = *reinterpret_cast<const int4*>(g.part + ((long)z * g.M + row) * 512 + col);
+      p[c].x += t.x; p[c].y += t.y; p[c].z += t.z; p[c].w += t.w;
+    }
+    r4[c] = *reinterpret_cast<const float4*>(g.res + row * 512 + col);
+    s4[c] = *reinterpret_cast<const float4*>(g.sw + col);
+    b4[c] = *reinterpret_cast<const float4*>(g.bias + col);
+  }
+  const float sr = g.sa[row];
+  float v[1][2][4];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int pa[4] = {p[c].x, p[c].y, p[c].z, p[c].w};
+    const float sw[4] = {s4[c].x, s4[c].y, s4[c].z, s4[c].w}, bb[4] = {b4[c].x, b4[c].y, b4[c].z, b4[c].w};
+    const float rr[4] = {r4[c].x, r4[c].y, r4[c].z, r4[c].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[0][c][e] = rr[e] + (((float)pa[e] * sr) * sw[e] + bb[e]);
+    *reinterpret_cast<float4*>(g.xout + row * 512 + 4 * (lane + 64 * c)) =
+        make_float4(v[0][c][0], v[0][c][1], v[0][c][2], v[0][c][3]);
+  }
+  float ga[2][4], gb[2][4];
+  ln_params512(g.ln_a, g.ln_b, lane, ga, gb);
+  ln_rows512<1>(v, ga, gb);
+  if (g.lnq) {
+    uint32_t qd[1][2];
+    float sc[1];
+    quant_rows512<1>(v, qd, sc);
+    *reinterpret_cast<uint32_t*>(g.lnq + kp_off(row, 4 * lane, 512)) = qd[0][0];
+    *reinterpret_cast<uint32_t*>(g.lnq + kp_off(row, 4 * (lane + 64), 512)) = qd[0][1];
+    if (lane == 0) g.lns[row] = sc[0];
+  } else {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      *reinterpret_cast<float4*>(g.lnout + row * 512 + 4 * (lane + 64 * c)) =
+          make_float4(v[0][c][0], v[0][c][1], v[0][c][2], v[0][c][3]);
+  }
 }
 
 hipError_t launch_gemm_row(const RowGemmArgs& g, hipStream_t st) {
@@ -731,6 +803,17 @@ hipError_t launch_gemm_row(const RowGemmArgs& g, hipStream_t st) {
   if (g.kp && (g.fault.kind != FK_NONE || g.K % 256)) return hipErrorInvalidValue;
   const dim3 grid((g.N / R_BN) * ((g.M + R_BM - 1) / R_BM)), block(512);
   const bool full = g.M % R_BM == 0;
+  if (g.epi == RE_RES_LN && g.kp && g.part && g.ksplit > 1 && g.fault.kind == FK_NONE) {
+    // split K: ksplit x the workgroups of a small M, then the row-wise epilogue
+    if ((g.K / 64) % (4 * g.ksplit)) return hipErrorInvalidValue;
+    const dim3 gs(grid.x, g.ksplit);
+    if (full) k_gemm_row<RE_PARTIAL, true, false, true><<<gs, block, 0, st>>>(g);
+    else k_gemm_row<RE_PARTIAL, false, false, true><<<gs, block, 0, st>>>(g);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    k_res_ln_partials<<<dim3((g.M + 3) / 4), dim3(256), 0, st>>>(g);
+    return hipGetLastError();
+  }
 #define QTX_ROW_LAUNCH(E)                                                                      \
   (g.fault.kind != FK_NONE ? (k_gemm_row<E, false, true, false><<<grid, block, 0, st>>>(g), 0)   \
    : g.kp ? (full ? (k_gemm_row<E, true, false, true><<<grid, block, 0, st>>>(g), 0)             \

@@ -119,7 +119,9 @@ hipError_t launch_attn_trace(const AttnArgs& a, float* qk, float* pc, hipStream_
 //   RE_RELU_PMAX        relu(y): per-row absmax of the tile -> pmax_out [N/512][M] (no y)
 //   RE_RELU_QUANT_PMAX  relu(y) quantized per token with the max over pmax_in [pmax_n][M]
 //                       -> out8 [M,N] (ld ldo8) + os [M]                 (FFN1, 2nd pass)
-enum RowEpi { RE_QUANT = 0, RE_RES_LN = 1, RE_RELU_PMAX = 2, RE_RELU_QUANT_PMAX = 3 };
+//   RE_PARTIAL          (internal: split-K RE_RES_LN at small M) the raw int32 accumulators
+//                       of K range blockIdx.y -> part + blockIdx.y * M * 512 [M,512]
+enum RowEpi { RE_QUANT = 0, RE_RES_LN = 1, RE_RELU_PMAX = 2, RE_RELU_QUANT_PMAX = 3, RE_PARTIAL = 4 };
 // Fault injected into one row-GEMM launch (the reference's fault models, qtx.h qtx_fault),
 // in GEMM-local coordinates:
 //   FK_INPUT   A[row, col] bit-flipped: acc[row, n] += (flip(a) - a) * W[n, col], n in [lo, hi)
@@ -152,6 +154,11 @@ struct RowGemmArgs {
   // per wait before giving up (0: the launcher's default).
   unsigned* status;
   int spin_limit;
+  // RE_RES_LN with kp at small M (at most 64 row tiles): split K over ksplit workgroups per
+  // tile (int32 partials into part [ksplit][M][512], >= ksplit * M * 2 KB), then one wave per
+  // row sums them and runs the residual + LayerNorm + quant epilogue.  0 / 1: no split.
+  int32_t* part;
+  int ksplit;
 };
 enum : unsigned { DEV_E_EXCHANGE_TIMEOUT = 1u };
 // W [N, K] int8 row-major -> KP layout with the row GEMM's column permutation per 512-wide
@@ -206,5 +213,7 @@ hipError_t launch_attention_mfma(const AttnArgs& a, hipStream_t st);
 hipError_t launch_attention_encq(const AttnArgs& a, int8_t* ctx8, float* sctx, hipStream_t st,
                                  bool force_encq = false, bool kp = false);
 hipError_t launch_fill_col(int64_t* ids, long bs, int B, int64_t val, hipStream_t st);
+// zero bytes (multiple of 16, 16-byte aligned) with a kernel (capturable into a hipGraph)
+hipError_t launch_zero(void* p, size_t bytes, hipStream_t st);
 
 }  // namespace qtx

@@ -547,6 +547,20 @@ hipError_t launch_step_inc(int* step, hipStream_t st) {
   return hipGetLastError();
 }
 
+// zero `n16` 16-byte chunks: used instead of hipMemsetAsync inside work that is captured
+// into a hipGraph (the decode prologue), where a captured memset did not re-run on replay
+__global__ void k_zero16(uint4* p, long n16) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16) p[i] = make_uint4(0, 0, 0, 0);
+}
+hipError_t launch_zero(void* p, size_t bytes, hipStream_t st) {
+  if (bytes % 16 || (reinterpret_cast<uintptr_t>(p) & 15)) return hipErrorInvalidValue;
+  const long n16 = (long)(bytes / 16);
+  if (n16 == 0) return hipSuccess;
+  k_zero16<<<dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, st>>>(reinterpret_cast<uint4*>(p), n16);
+  return hipGetLastError();
+}
+
 __global__ void k_fill_col(int64_t* ids, long bs, int B, int64_t val) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B) ids[b * bs] = val;

@@ -2005,7 +2005,7 @@ hipError_t launch_gemm_wsx(const RowGemmArgs& g, hipStream_t st) {
   // u64 granules + the ticket counter (padded: a memset of a multiple of 16 bytes), zeroed
   // before every launch
   const long ngran = 4L * 32 * nb + 2;
-  hipError_t e = hipMemsetAsync(g.pmax_out, 0, (size_t)ngran * 8, st);
+  hipError_t e = launch_zero(g.pmax_out, (size_t)ngran * 8, st);   // (a kernel: graph-capturable)
   if (e != hipSuccess) return e;
   RowGemmArgs a = g;
   if (!a.status)                              // the u32 after the ticket counter

@@ -39,7 +39,8 @@ class RowGemm(C.Structure):
                 ("out8", P), ("ldo8", I64), ("o8_ts", I64), ("os", P), ("os_ts", I64),
                 ("res", P), ("xout", P), ("ln_a", P), ("ln_b", P),
                 ("lnq", P), ("lns", P), ("lnout", P),
-                ("pmax_out", P), ("pmax_in", P), ("pmax_n", I32), ("kp", I32), ("status", P)]
+                ("pmax_out", P), ("pmax_in", P), ("pmax_n", I32), ("kp", I32), ("status", P),
+                ("part", P), ("ksplit", I32)]
 
 class Fault(C.Structure):
     """struct qtx_fault (include/qtx.h)."""

@@ -456,6 +456,42 @@ def test_linear_rows_ws_ffn1_onepass_scales(torch, M, wsy, monkeypatch):
     assert status == 0
 
 
+@pytest.mark.parametrize("M,ks,lnq", [(7, 4, True), (300, 4, True), (2304, 4, True),
+                                      (300, 2, True), (300, 8, True), (129, 4, False),
+                                      (8192, 4, True)])
+def test_linear_rows_res_ln_splitk(torch, oracle_model, M, ks, lnq):
+    """FFN2 (epi 1, kp = 1, K = 2048) with K split over ks workgroups per row tile (int32
+    partials, then the row-wise residual + LayerNorm + quant epilogue): bit-exact against the
+    oracle, for the quantized KP output and the fp32 LayerNorm output (the encoder's last
+    layer), ragged M included."""
+    from qtx._lib import lib
+    rng = np.random.default_rng(M + 7 * ks)
+    qh, sh = O.quant_rows(np.maximum(rng.standard_normal((M, 2048)), 0).astype(f32))
+    qw, sw = O.quant_weight((rng.standard_normal((512, 2048)) * 0.05).astype(f32), 8)
+    wk = torch.empty((512, 2048), dtype=torch.int8, device="cuda")
+    assert lib().qtx_pack_w_kp(P(dev(torch, qw)), 512, 2048, P(wk), S0) == 0
+    b = rng.standard_normal(512).astype(f32)
+    res = (rng.standard_normal((M, 512)) * 2).astype(f32)
+    la, lb = oracle_model.dec[1]["ln"][0]
+    xd = dev(torch, res.copy())
+    part = torch.empty((ks * M * 512,), dtype=torch.int32, device="cuda")
+    out = dict(lnq=torch.zeros((M + (M & 1), 512), dtype=torch.int8, device="cuda"),
+               lns=torch.empty(M, dtype=torch.float32, device="cuda")) if lnq else \
+        dict(lnout=torch.empty((M, 512), dtype=torch.float32, device="cuda"))
+    _rows_call(torch, A=dev(torch, _to_kp(qh)), sa=dev(torch, sh), W=wk, sw=dev(torch, sw),
+               bias=dev(torch, b), M=M, N=512, K=2048, epi=1, res=xd, xout=xd,
+               ln_a=dev(torch, la), ln_b=dev(torch, lb), kp=1, part=part, ksplit=ks, **out)
+    x = res + O.linear_epilogue(O.int_gemm(qh, qw), sh, sw, b)
+    np.testing.assert_array_equal(xd.cpu().numpy(), x)
+    ln = O.layer_norm(x, la, lb)
+    if lnq:
+        q, s2 = O.quant_rows(ln)
+        np.testing.assert_array_equal(_from_kp(out["lnq"].cpu().numpy(), M), q)
+        np.testing.assert_array_equal(out["lns"].cpu().numpy(), s2)
+    else:
+        np.testing.assert_array_equal(out["lnout"].cpu().numpy(), ln)
+
+
 def _ws_pack_ref(w):
     """The WS order of qtx_pack_w_ws (include/qtx.h), restated in numpy: 1 KB block
     ((t*8 + w)*8 + s)*4 + j, lane l: W[512t + 64w + 16((l & 15) >> 2) + 4j + (l & 3)]
