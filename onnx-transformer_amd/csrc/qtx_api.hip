@@ -1005,7 +1005,6 @@ struct GreedyWS {
   int* gsteps;
   int64_t* ids;       // [B][max_len] the decode writes here; copied out to the caller's ids
   uint8_t* mask;      // [B][S] staged copy of the caller's src_mask
-  int64_t* src;       // [B][S] staged copy of the caller's src ids (the prologue graph's input)
 };
 
 // Sub-batch split of the fused decode.  Sentences are independent (per-token quantization:
@@ -1053,7 +1052,6 @@ GreedyWS carve_greedy(Arena& ar, const qtx_config& c, int B, int S, int max_len)
   g.gsteps = ar.take<int>(4 * QTX_MAX_GROUPS);
   g.ids = ar.take<int64_t>((size_t)B * max_len);
   g.mask = ar.take<uint8_t>((size_t)B * S);
-  g.src = ar.take<int64_t>((size_t)B * S);
   return g;
 }
 
@@ -1473,77 +1471,18 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
   int64_t* ids = g.ids;
   const bool fused = S <= 128 && max_len <= 128 && !env_flag("QTX_UNFUSED");
 
-  // the prologue: memory = encode(src_embed(src), src_mask), the cross K/V of every layer,
-  // ids[:, 0] = start, step[0] = position 0, step[1] = arrival counter
-  const char* pp = getenv("QTX_PRE_PART");       // diagnostic: 1 encoder only, 2 cross K/V only
-  const int part = pp && *pp ? atoi(pp) : 0;
-  auto prologue_a = [&](const int64_t* sp, hipStream_t s) -> int {
-    HIPCHK(launch_embed(sp, S, B, S, nullptr, 0, m->src_lut, c.src_vocab, m->pe, c.max_len,
-                        g.enc.x, (long)S * D, s));
-    RC(encoder_run(m, g.enc.x, src_mask, B, S, g.memory, g.enc, s, f));
-    return QTX_OK;
-  };
-  auto prologue_b = [&](hipStream_t s) -> int {
-    RC(cross_kv(m, g.memory, B * S, g.cross, s));
-    HIPCHK(launch_fill_col(ids, max_len, B, start, s));
-    HIPCHK(launch_zero(g.step, 16, s));
-    return QTX_OK;
-  };
-  auto prologue = [&](const int64_t* sp, hipStream_t s) -> int {
-    if (part != 2) RC(prologue_a(sp, s));
-    if (part != 1) RC(prologue_b(s));
-    return QTX_OK;
-  };
-  // Fused decodes replay the prologue as a hipGraph too (captured once per shape and
-  // workspace, on the staged src): ~40 launches whose host enqueue (~10 us each) the
-  // GPU otherwise waits for at the decode's start.  Experiment (QTX_PRE_GRAPH=1), off by
-  // default.
-  const bool pre_graph = fused && (!f || f->kind == QTX_FAULT_NONE) && !env_flag("QTX_NO_GRAPH") &&
-                         env_flag("QTX_PRE_GRAPH");
-  if (!pre_graph) {
-    RC(prologue(src, st));
-  } else {
-    qtx_model* mm = const_cast<qtx_model*>(m);
-    std::lock_guard<std::mutex> lock(mm->mu);
-    DeviceGuard dg(mm->device);
-    HIPCHK(hipMemcpyAsync(g.src, src, (size_t)B * S * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-    if (part == 2) RC(prologue_a(g.src, st));
-    if (!mm->gstream[0]) {
-      HIPCHK(hipStreamCreateWithFlags(&mm->gstream[0], hipStreamNonBlocking));
-      HIPCHK(hipEventCreateWithFlags(&mm->ev_out[0], hipEventDisableTiming));
-    }
-    std::string variant;
-    for (const char* k : {"QTX_WSQ", "QTX_WSY", "QTX_WSR", "QTX_NO_SPLITK", "QTX_NO_KP", "QTX_NO_WSX",
-                          "QTX_WS_NOPIPE", "QTX_NO_ATTN_ENCQ", "QTX_WS_MIN_M", "QTX_PRE_PART"}) {
-      const char* v = getenv(k);
-      variant += std::string(k) + "=" + (v ? v : "") + ";";
-    }
-    const GraphKey key{B, S, max_len, -1, g.gsteps, variant};
-    auto it = mm->graphs.find(key);
-    if (it == mm->graphs.end()) {
-      if (mm->graphs.size() >= 16) mm->clear_graphs();
-      hipGraph_t graph = nullptr;
-      HIPCHK(hipStreamBeginCapture(mm->gstream[0], hipStreamCaptureModeThreadLocal));
-      const int rc = prologue(g.src, mm->gstream[0]);
-      const hipError_t e = hipStreamEndCapture(mm->gstream[0], &graph);
-      if (rc != QTX_OK || e != hipSuccess) {
-        if (graph) (void)hipGraphDestroy(graph);
-        if (rc != QTX_OK) return rc;
-        HIPCHK(e);
-      }
-      hipGraphExec_t exec = nullptr;
-      const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(graph);
-      HIPCHK(ei);
-      GraphEntry ent;
-      ent.execs.push_back(exec);
-      it = mm->graphs.emplace(key, std::move(ent)).first;
-    }
-    HIPCHK(hipGraphLaunch(it->second.execs[0], st));
-    if (!it->second.done) HIPCHK(hipEventCreateWithFlags(&it->second.done, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(it->second.done, st));
-    if (part == 1) RC(prologue_b(st));
-  }
+  // encoder: memory = encode(src_embed(src), src_mask); the cross K/V of every layer
+  // (captured into a hipGraph with the steps' replay — QTX_PRE_GRAPH in round 3 — it
+  // measured no faster: 14.34 vs 14.31 ms per B = 32 decode; the host's enqueue of these
+  // launches runs ahead of the GPU)
+  HIPCHK(launch_embed(src, S, B, S, nullptr, 0, m->src_lut, c.src_vocab, m->pe, c.max_len,
+                      g.enc.x, (long)S * D, st));
+  RC(encoder_run(m, g.enc.x, src_mask, B, S, g.memory, g.enc, st, f));
+  RC(cross_kv(m, g.memory, B * S, g.cross, st));
+
+  // ids[:, 0] = start ; step[0] = position 0, step[1] = arrival counter
+  HIPCHK(launch_fill_col(ids, max_len, B, start, st));
+  HIPCHK(launch_zero(g.step, 16, st));
   if (!fused) {
     for (int t = 0; t + 1 < max_len; ++t) RC(greedy_step_unfused(m, g, B, S, max_len, ids, src_mask, st));
     return QTX_OK;
