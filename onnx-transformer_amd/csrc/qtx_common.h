@@ -34,6 +34,8 @@ static __device__ unsigned long long* qtx_stamp_buf;
   } while (0)
 // accumulated phase times: QTX_NOW() reads the clock, QTX_STAMP_VAL stores a value
 #define QTX_NOW() ((long long)__builtin_amdgcn_s_memtime())
+// the constant 100 MHz clock: in-kernel clock = delta(QTX_NOW) / delta(QTX_RNOW) x 100 MHz
+#define QTX_RNOW() ((long long)__builtin_amdgcn_s_memrealtime())
 #define QTX_STAMP_VAL(slot, v)                                                          \
   do {                                                                                    \
     if (threadIdx.x == 0 && qtx_stamp_buf)                                                \
@@ -45,6 +47,7 @@ static __device__ unsigned long long* qtx_stamp_buf;
   do {                  \
   } while (0)
 #define QTX_NOW() 0LL
+#define QTX_RNOW() 0LL
 #define QTX_STAMP_VAL(slot, v) \
   do {                         \
   } while (0)

@@ -767,6 +767,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   float* const sal = red0 + 2 * 8 * WP_R;                    // [2][8 waves][64]: row scales
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int f = lane & 15, gq = lane >> 4;
+  const long long rt_entry = QTX_RNOW();          // QTX_STAMPS builds: kernel entry
   const int nsl = g.N >> 9;
   const int wpt = gridDim.x / nsl;
   int t = blockIdx.x % nsl, r0 = blockIdx.x / nsl;
@@ -944,7 +945,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   v4i acc[2][4];
   float y[2][16];
   long long st_top = 0, st_mm = 0, st_y = 0;          // QTX_STAMPS builds only
-  const long long st_0 = QTX_NOW();
+  const long long st_0 = QTX_NOW(), rt_0 = QTX_RNOW();
   // ---- block 0: MFMAs, then its y
   __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
   __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
@@ -999,6 +1000,9 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   QTX_STAMP_VAL(5, QTX_NOW() - st_0);
+  QTX_STAMP_VAL(7, QTX_RNOW() - rt_0);
+  QTX_STAMP_VAL(8, rt_entry);
+  QTX_STAMP_VAL(9, QTX_RNOW());
 }
 
 // =====================================================================================

@@ -42,9 +42,11 @@ def main():
         setattr(args, k, v.data_ptr() if hasattr(v, "data_ptr") else v)
     for wsq in ("0", "1"):
         os.environ["QTX_WSQ"] = wsq
-        for _ in range(3):
-            buf.zero_()
+        # >= 2 s of back-to-back launches first: the clock the chip holds under this load
+        # (MI355X_MICROARCH.md, DVFS give-back item 6)
+        for _ in range(3000):
             _lib.call("qtx_linear_rows", C.byref(args), st)
+        buf.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         _lib.call("qtx_linear_rows", C.byref(args), st)
@@ -58,7 +60,15 @@ def main():
         print(f"QTX_WSQ={wsq}: {e0.elapsed_time(e1) * 1e3:.1f} us (stamped), {len(s)} WGs x {nb:.0f} blocks; "
               f"median cycles: prologue+block0 {med(0):.0f}; per block: top wait {per(1):.0f}, "
               f"[wsp: half1 {per(2):.0f}, mid barrier {per(3):.0f}, half2 {per(4):.0f}] "
-              f"[wsq: mfma+quant {per(2):.0f}, y {per(4):.0f}]; total {med(5):.0f}", flush=True)
+              f"[wsq: mfma+quant {per(2):.0f}, y {per(4):.0f}]; total {med(5):.0f}"
+              + (f"; in-kernel clock {float(np.median(s[:, 5] / np.maximum(s[:, 7], 1))) * 100:.0f} MHz"
+                 if wsq == "1" else ""), flush=True)
+        if wsq == "1":      # absolute entry / exit on the 100 MHz clock (s_memrealtime)
+            t0, t1 = s[:, 8], s[:, 9]
+            print(f"   workgroup entry spread {(t0.max() - t0.min()) / 100:.2f} us, exit spread "
+                  f"{(t1.max() - t1.min()) / 100:.2f} us, first entry to last exit "
+                  f"{(t1.max() - t0.min()) / 100:.2f} us, median workgroup lifetime "
+                  f"{np.median(t1 - t0) / 100:.2f} us", flush=True)
         if wsq == "1":      # per wave of WG 0..: top wait / MFMA+quant / y per block, median over WGs
             pw = buf.cpu().numpy().reshape(-1)[256 * 16:256 * 16 + 256 * 8 * 4].reshape(256, 8, 4).astype(np.int64)
             pw = pw[pw[:, 0, 3] > 1]
