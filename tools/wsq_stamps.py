@@ -40,7 +40,7 @@ def main():
     for k, v in dict(A=a, sa=sa, W=wk, sw=sw, bias=bias, M=M, N=3 * D, K=D, kp=2, epi=0,
                      out8=out8, ldo8=D, o8_ts=M * D, os=os_, os_ts=M).items():
         setattr(args, k, v.data_ptr() if hasattr(v, "data_ptr") else v)
-    for wsq in ("0", "1"):
+    for wsq in sys.argv[1:] or ("0", "1"):
         os.environ["QTX_WSQ"] = wsq
         # >= 2 s of back-to-back launches first: the clock the chip holds under this load
         # (MI355X_MICROARCH.md, DVFS give-back item 6)
