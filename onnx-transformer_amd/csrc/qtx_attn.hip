@@ -478,9 +478,13 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
     // head h - 2 in iteration h - 1) and read by the PV of head h in iteration h + 1: one
     // barrier at the top of each iteration orders both
     float xp[8][4];
+    long long st_bar = 0;                          // QTX_STAMPS builds only: barrier wait
     static_for<9>([&](auto hc) {
       constexpr int h = decltype(hc)::value;
+      const long long tb0 = QTX_NOW();
       __syncthreads();
+      st_bar += QTX_NOW() - tb0;
+      QTX_STAMP(4 + h);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (h < 8) convert_v(std::integral_constant<int, (h < 8 ? h : 0)>{});
       float xn[8][4];
@@ -497,6 +501,10 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
           for (int e = 0; e < 4; ++e) xp[kt][e] = xn[kt][e];
       }
     });
+#ifdef QTX_STAMPS
+    // per wave (lane 0): barrier wait over the head loop, at [4096 + 2 (8 block + wave)]
+    if (lane == 0 && qtx_stamp_buf) qtx_stamp_buf[4096 + 2 * (b * 8 + wave)] = st_bar;
+#endif
   }
   QTX_STAMP(2);
 
