@@ -1790,14 +1790,19 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
   __builtin_amdgcn_s_barrier();
   // iteration k; yb / mb: the buffers of blocks of k's parity (block k-2 in, block k out),
   // mo: the slice maximum of block k-1 (the other parity)
+  long long st_top = 0, st_fm = 0, st_mm = 0, st_y = 0;   // QTX_STAMPS builds only
+  const long long st_0 = QTX_NOW();
   auto iter = [&](int k, float (&yb)[2][16], float& mb, float& mo) {
+    const long long t0 = QTX_NOW();
     if (k > 0) {
       __builtin_amdgcn_s_waitcnt(WAIT_VM(3));   // block k's DMA retired (behind: 3 stores)
       __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
       __builtin_amdgcn_s_barrier();
     }
+    const long long t1 = QTX_NOW();
     float m2 = 0.0f;
     if (k >= 2) m2 = full_max(k - 2, mb);       // granule loads: before this iteration's DMA
+    const long long t2 = QTX_NOW();
     if (k >= 1 && k <= nblk) {
       mo = slice_max(k - 1);
       publish(k - 1, mo);
@@ -1806,7 +1811,14 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
     if (k < nblk) {
       if (k >= 2) mfma_block(acc, k, T_, k - 2, yb, m2);
       else mfma_block(acc, k, F_, 0, yb, 0.0f);
+      const long long t3 = QTX_NOW();
       form_y(acc, yb, k);
+      if (k >= 2) {
+        st_top += t1 - t0;
+        st_fm += t2 - t1;
+        st_mm += t3 - t2;
+        st_y += QTX_NOW() - t3;
+      }
     } else if (k >= 2) {
       quant_all(k - 2, yb, m2);
     } else {
@@ -1818,6 +1830,16 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
     if (k + 1 <= nblk + 1) iter(k + 1, y1, mq1, mq0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  QTX_STAMP_VAL(5, QTX_NOW() - st_0);
+  QTX_STAMP_VAL(6, nblk);
+#ifdef QTX_STAMPS
+  // per wave (lane 0): top wait, partners' maxima, MFMA + quantization, y over blocks 2..,
+  // at [256 * 16 + (block * 8 + wave) * 8 + phase]
+  if (lane == 0 && qtx_stamp_buf) {
+    unsigned long long* pw = qtx_stamp_buf + 256 * 16 + ((long)blockIdx.x * 8 + wave) * 8;
+    pw[0] = st_top; pw[1] = st_fm; pw[2] = st_mm; pw[3] = st_y; pw[4] = nblk;
+  }
+#endif
 }
 
 // =====================================================================================

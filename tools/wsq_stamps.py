@@ -77,5 +77,55 @@ def main():
                 print(f"   wave {w}: top wait {per_w[w, 0]:.0f}, mfma+quant {per_w[w, 1]:.0f}, y {per_w[w, 2]:.0f}")
 
 
+def ffn1():
+    """k_gemm_wsy (the one-pass FFN1, kp = 3) at cfg3: per-wave phase cycles per block."""
+    import torch
+    from qtx import _lib
+    raw = C.CDLL(STAMP_LIB)
+    buf = torch.zeros((4096, 16), dtype=torch.int64, device="cuda")
+    raw.qtx_debug_set_stamps_ws(C.c_void_p(buf.data_ptr()))
+    M, D, N = 32768, 512, 2048
+    rng = np.random.default_rng(0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    a = T(rng.integers(-127, 128, (M, D)).astype(np.int8))
+    sa = torch.full((M,), 0.01, device="cuda")
+    sw = torch.full((N,), 0.01, device="cuda")
+    bias = torch.zeros(N, device="cuda")
+    h8 = torch.empty((M, N), dtype=torch.int8, device="cuda")
+    sh = torch.empty((M,), device="cuda")
+    gx = torch.empty(((32 * M + 2048) // 4,), dtype=torch.float32, device="cuda")
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    w = T(rng.integers(-127, 128, (N, D)).astype(np.int8))
+    wk = torch.empty_like(w)
+    _lib.call("qtx_pack_w_ws", C.c_void_p(w.data_ptr()), N, D, C.c_void_p(wk.data_ptr()), st)
+    args = _lib.RowGemm()
+    for k, v in dict(A=a, sa=sa, W=wk, sw=sw, bias=bias, M=M, N=N, K=D, kp=3, epi=3,
+                     pmax_out=gx, out8=h8, ldo8=N, os=sh).items():
+        setattr(args, k, v.data_ptr() if hasattr(v, "data_ptr") else v)
+    for _ in range(2000):
+        _lib.call("qtx_linear_rows", C.byref(args), st)
+    buf.zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    _lib.call("qtx_linear_rows", C.byref(args), st)
+    e1.record()
+    torch.cuda.synchronize()
+    s = buf.cpu().numpy()[:256].astype(np.int64)
+    s = s[s[:, 5] > 0]
+    nb = float(np.median(s[:, 6]))
+    print(f"FFN1 k_gemm_wsy: {e0.elapsed_time(e1) * 1e3:.1f} us (stamped), {len(s)} WGs x {nb:.0f} blocks, "
+          f"median total {np.median(s[:, 5]):.0f} cycles ({np.median(s[:, 5]) / nb:.0f} per block)")
+    pw = buf.cpu().numpy().reshape(-1)[256 * 16:256 * 16 + 256 * 8 * 8].reshape(256, 8, 8).astype(np.int64)
+    pw = pw[pw[:, 0, 4] > 2]
+    per_w = np.median(pw[:, :, :4] / (pw[:, :, 4:5] - 2), axis=0)
+    for w in range(8):
+        print(f"   wave {w}: top wait {per_w[w, 0]:.0f}, partner maxima {per_w[w, 1]:.0f}, "
+              f"mfma+quant {per_w[w, 2]:.0f}, y {per_w[w, 3]:.0f}")
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["ffn1"]:
+        os.environ["QTX_LIB_PATH"] = STAMP_LIB
+        ffn1()
+        sys.exit(0)
     main()
