@@ -183,6 +183,27 @@ def pmc_traffic():
     return None
 
 
+def profiler_dominant(B, alg):
+    """The dominant kernel's average per-dispatch duration at the decode grid in the newest
+    committed rocprofv3 kernel stats of this bench (tools/prof_summary.py "by launch grid"
+    table), with the roofline fraction it implies — the profiler's view next to the live
+    HIP-event figure, or None when no profile lists the kernel at that grid."""
+    import glob
+    grid = f"{(D // 16) * 256}x{(B + 3) // 4}"          # 16 columns x 4 rows per workgroup
+    for fn in sorted(glob.glob(os.path.join(REPO, "profiles", "*_bench_kernel_stats.md")), reverse=True):
+        with open(fn) as f:
+            for line in f:
+                cells = [c.strip() for c in line.split("|")]
+                if len(cells) > 6 and DOMINANT in cells[1] and cells[2].startswith(grid + " "):
+                    us = float(cells[5])
+                    return {"source": os.path.relpath(fn, REPO), "avg_us": us,
+                            "achieved": alg / (us * 1e-6) / 1e9, "frac": alg / (us * 1e-6) / PEAK_HBM,
+                            "note": "rocprofv3 per-dispatch durations of the graph-replayed "
+                                    "decode kernels; the profiler serializes graph dispatches, "
+                                    "so they read longer than the live per-node time"}
+    return None
+
+
 def _quantized_rows(rng, M, K, relu=False):
     """int8 rows distributed as the encoder's activations: per-token absmax quantization
     (quant_linear.py:30-43) of Gaussian rows (LayerNorm outputs), or of ReLU'd Gaussian
@@ -454,6 +475,7 @@ def main():
                 "unit": "GB/s", "frac": alg / kt / PEAK_HBM, "traffic": pmc_traffic(),
                 "avg_us": kt * 1e6, "empty_node_us": nop_us,
                 "marginal_us": chain_us - nop_us, "alg_bytes_per_launch": alg,
+                "profiler": profiler_dominant(Bd, alg),
                 "method": f"hipGraph chain of 256 dependent launches over {DOMINANT_COPIES} "
                           "rotating operand sets, HIP events on the replay stream: us per node "
                           "(launch boundary included); empty_node_us = the same chain of empty "
