@@ -86,6 +86,37 @@ __device__ __forceinline__ float wave_max(float v) {
   return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 
+// wave_sum / wave_max of R values at once, level by level: the R DPP chains interleave
+// instead of each waiting out its own DPP and readlane latencies (the compiler kept
+// per-value calls serial, with s_nop between dependent DPP adds).  Bit-identical to R calls.
+template <int R>
+__device__ __forceinline__ void wave_sum_n(float (&v)[R]) {
+#pragma unroll
+  for (int j = 0; j < R; ++j) v[j] = v[j] + dpp<0xB1>(v[j]);
+#pragma unroll
+  for (int j = 0; j < R; ++j) v[j] = v[j] + dpp<0x4E>(v[j]);
+#pragma unroll
+  for (int j = 0; j < R; ++j) v[j] = v[j] + dpp<0x141>(v[j]);
+#pragma unroll
+  for (int j = 0; j < R; ++j) v[j] = v[j] + dpp<0x140>(v[j]);
+#pragma unroll
+  for (int j = 0; j < R; ++j) v[j] = (lane_f(v[j], 0) + lane_f(v[j], 16)) + (lane_f(v[j], 32) + lane_f(v[j], 48));
+}
+template <int R>
+__device__ __forceinline__ void wave_max_n(float (&v)[R]) {
+#pragma unroll
+  for (int j = 0; j < R; ++j) v[j] = fmaxf(v[j], dpp<0xB1>(v[j]));
+#pragma unroll
+  for (int j = 0; j < R; ++j) v[j] = fmaxf(v[j], dpp<0x4E>(v[j]));
+#pragma unroll
+  for (int j = 0; j < R; ++j) v[j] = fmaxf(v[j], dpp<0x141>(v[j]));
+#pragma unroll
+  for (int j = 0; j < R; ++j) v[j] = fmaxf(v[j], dpp<0x140>(v[j]));
+#pragma unroll
+  for (int j = 0; j < R; ++j)
+    v[j] = fmaxf(fmaxf(lane_f(v[j], 0), lane_f(v[j], 16)), fmaxf(lane_f(v[j], 32), lane_f(v[j], 48)));
+}
+
 // The same trees restricted to each 16-lane DPP row: every lane of the row gets the row's
 // canonical sum / max (the first four levels of wave_sum).
 __device__ __forceinline__ float row16_sum(float v) {
@@ -188,6 +219,23 @@ __device__ __forceinline__ float div_const(float a, float b) {
   if (__builtin_expect(__ballot(!div_ok(a)) == 0ull, 1)) return div_cr(a, b, y);
   return a / b;
 }
+// R of them in place behind ONE wave-uniform vote (the true division for all R when any
+// is out of range: it equals div_cr wherever div_cr is exact, so the values are those of
+// R div_const calls)
+template <int R>
+__device__ __forceinline__ void div_const_n(float (&a)[R], float b) {
+  const float y = 1.0f / b;
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < R; ++j) bad |= !div_ok(a[j]);
+  if (__builtin_expect(__ballot(bad) == 0ull, 1)) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) a[j] = div_cr(a[j], b, y);
+  } else {
+#pragma unroll
+    for (int j = 0; j < R; ++j) a[j] = a[j] / b;
+  }
+}
 
 // ---------------------------------------------------------------- quantizer
 // quant_linear.py:30-43 / :5-17:  s = max(absmax, 1e-5) / qmax;  q = rint(x / s).
@@ -277,8 +325,9 @@ __device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float (&ga
         if (c | e) s = s + v[j][c][e];
     mean[j] = s;
   }
+  wave_sum_n<R>(mean);
 #pragma unroll
-  for (int j = 0; j < R; ++j) mean[j] = wave_sum(mean[j]) / 512.0f;
+  for (int j = 0; j < R; ++j) mean[j] = mean[j] / 512.0f;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
 #pragma unroll
@@ -293,11 +342,17 @@ __device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float (&ga
         if (c | e) ss = ss + v[j][c][e] * v[j][c][e];
     den[j] = ss;
   }
+  wave_sum_n<R>(den);
+  div_const_n<R>(den, 511.0f);
 #pragma unroll
-  for (int j = 0; j < R; ++j) den[j] = sqrtf(div_const(wave_sum(den[j]), 511.0f)) + 1e-6f;
+  for (int j = 0; j < R; ++j) den[j] = sqrtf(den[j]) + 1e-6f;
   // y = (a * d) / den + b, the division correctly rounded via div_cr (one true division
-  // per row for the reciprocal), true division if any value is outside div_cr's range
-  DivRange rg;
+  // per row for the reciprocal), true division if any value is outside div_cr's range.
+  // The range guard costs 2 VALU per value: max |a| on bit patterns (NaN / inf fail it) and
+  // min |a| as floats (v_max3 / v_min3 pairs); a zero numerator fails the fast guard too,
+  // and then DivRange's zero-exempt check (4 VALU per value) decides, off the common path.
+  uint32_t mx = 0u;
+  float mn = __builtin_inff();
 #pragma unroll
   for (int j = 0; j < R; ++j) {
 #pragma unroll
@@ -305,12 +360,24 @@ __device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float (&ga
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         v[j][c][e] = ga[c][e] * v[j][c][e];     // numerator a * d
-        rg.add(v[j][c][e]);
+        mx = max(mx, __float_as_uint(v[j][c][e]) & 0x7fffffffu);
+        mn = fminf(mn, fabsf(v[j][c][e]));
       }
   }
-  bool ok = rg.ok();
+  bool dok = true;
 #pragma unroll
-  for (int j = 0; j < R; ++j) ok &= divisor_ok(den[j]);
+  for (int j = 0; j < R; ++j) dok &= divisor_ok(den[j]);
+  bool ok = dok && mx < 0x5d800000u && mn > 0x1p-60f;
+  if (__builtin_expect(__ballot(!ok) != 0ull, 0)) {
+    DivRange rg;
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) rg.add(v[j][c][e]);
+    ok = dok && rg.ok();
+  }
   if (__builtin_expect(__ballot(!ok) == 0ull, 1)) {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -349,23 +416,51 @@ __device__ __forceinline__ void ln_rows512(float (&v)[R][2][4], const float* a, 
   ln_rows512<R>(v, ga, gb);
 }
 
-// per-token quantization of R rows (2 float4 per lane each) into int8 dwords + scales
+// per-token quantization of R rows (2 float4 per lane each) into int8 dwords + scales:
+// rint(x / s) as quant_pack computes it, for all R rows behind ONE near-tie vote.  The tie
+// test reuses the biased rint: t = RN(r + 1.5 * 2^23), d = r - (t - 1.5 * 2^23) (both
+// subtractions exact for |r| < 2^22) is r's distance to the nearest integer, and
+// |d| > 0.5 - 2^-13 is exactly quant_pack's |frac(r) - 0.5| < 2^-13; one v_max3 per two
+// values folds it (4.5 VALU per value with the rint, against 6).
 template <int R>
 __device__ __forceinline__ void quant_rows512(const float (&v)[R][2][4], uint32_t (&q)[R][2],
                                               float (&sc)[R]) {
-  float am[R];
 #pragma unroll
   for (int j = 0; j < R; ++j) {
-    am[j] = 0.0f;
+    sc[j] = 0.0f;
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) am[j] = fmaxf(am[j], fabsf(v[j][c][e]));
+      for (int e = 0; e < 4; ++e) sc[j] = fmaxf(sc[j], fabsf(v[j][c][e]));
+  }
+  wave_max_n<R>(sc);
+#pragma unroll
+  for (int j = 0; j < R; ++j) sc[j] = fmaxf(sc[j], 1e-5f);
+  div_const_n<R>(sc, 127.0f);                     // quant_scale of each row
+  constexpr float BIAS = 12582912.0f;
+  float t[R][8];
+  float dm = 0.0f;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const float inv = __builtin_amdgcn_rcpf(sc[j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float r = v[j][i >> 2][i & 3] * inv;
+      t[j][i] = r + BIAS;
+      dm = fmaxf(dm, fabsf(r - (t[j][i] - BIAS)));
+    }
+  }
+  if (__builtin_expect(__ballot(dm > 0.5f - 0x1p-13f) != 0ull, 0)) {
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[j][i] = v[j][i >> 2][i & 3] / sc[j] + BIAS;
   }
 #pragma unroll
-  for (int j = 0; j < R; ++j) sc[j] = quant_scale(wave_max(am[j]), 127.0f);
-#pragma unroll
-  for (int j = 0; j < R; ++j) quant_pack<8>(&v[j][0][0], sc[j], q[j]);
+  for (int j = 0; j < R; ++j) {
+    q[j][0] = pack4_biased(t[j][0], t[j][1], t[j][2], t[j][3]);
+    q[j][1] = pack4_biased(t[j][4], t[j][5], t[j][6], t[j][7]);
+  }
 }
 
 }  // namespace qtx

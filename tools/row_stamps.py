@@ -24,7 +24,7 @@ def main():
     raw = C.CDLL(STAMP_LIB)
     buf = torch.zeros((4096, 16), dtype=torch.int64, device="cuda")
     raw.qtx_debug_set_stamps_gemm(C.c_void_p(buf.data_ptr()))
-    M, D, F = 32768, 512, 2048
+    M, D, F = int(os.environ.get("QTX_STAMP_M", "32768")), 512, 2048
     rng = np.random.default_rng(0)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     sa = torch.full((M,), 0.01, device="cuda")
