@@ -53,6 +53,28 @@ def encoder_gemm_ops(B, S, n_layers=6):
     return n_layers * 2 * M * (3 * D * D + D * D + D * F + F * D)
 
 
+def gemm_roofline_us(M):
+    """Roofline bound of each QuantLinear launch of one encoder layer at M rows: max(MFMA
+    time at the dense int8 peak, algorithmic HBM bytes at 8 TB/s).  Bytes: int8 A and W,
+    fp32 row scales in/out, per-channel scale + bias, the int8 codes written; O and FFN2 also
+    read the fp32 residual and write x (sublayer_connection.py:17) — the fp32 residual
+    stream makes them HBM-bound whatever the GEMM does."""
+    row = 4 * M                                   # one fp32 scale per row
+    shapes = {  # name: (N, K, bytes besides A, W, sw/bias)
+        "qkv_quant": (3 * D, D, 3 * (M * D + row)),
+        "o_res_ln": (D, D, 2 * 4 * M * D + M * D + row + 8 * D),
+        "ffn1_quant_onepass": (F, D, M * F + row),
+        "ffn2_res_ln": (D, F, 2 * 4 * M * D + M * D + row + 8 * D)}
+    out = {}
+    for k, (N, K, extra) in shapes.items():
+        by = M * K + row + N * K + 8 * N + extra
+        out[k] = {"mfma_us": 2 * M * N * K / PEAK_INT8_OPS * 1e6, "hbm_us": by / PEAK_HBM * 1e6,
+                  "alg_bytes": by}
+        out[k]["bound_us"] = max(out[k]["mfma_us"], out[k]["hbm_us"])
+        out[k]["bound"] = "mfma" if out[k]["mfma_us"] >= out[k]["hbm_us"] else "hbm"
+    return out
+
+
 # The decode step's dominant kernel class (most time per cfg2 step in the rocprofv3 kernel
 # stats, profiles/r02q_bench_kernel_stats.md "by launch grid", B = 32 grids: 12 launches per
 # step x 4.60 us = 55 us, ahead of cross-attention 31 and FFN2 33): the attention output
@@ -542,6 +564,16 @@ def main():
                 # within 2 %, profiles/r02j_pmc_encoder.json's note)
                 "gemm_us_per_layer": {k: round(t, 1) for k, (t, _) in g.items()},
                 "frac_of_int8_peak_quantlinear_gemms": gemm_ops / (gemm_us * 1e-6) / PEAK_INT8_OPS}
+            # each launch against its own roofline (max of MFMA and HBM time): O and FFN2
+            # carry the fp32 residual stream, so the int8 peak fraction the layer can reach
+            # at all is sum(ops) / sum(bounds) / peak (0.57 at 8 TB/s)
+            rf = gemm_roofline_us(Bc * Sc)
+            bound_us = sum(r["bound_us"] for r in rf.values())
+            out["cfg3_encoder"]["roofline_us_per_layer"] = {
+                k: {"bound": r["bound"], "bound_us": round(r["bound_us"], 1),
+                    "frac": round(r["bound_us"] / g[k][0], 3)} for k, r in rf.items()}
+            out["cfg3_encoder"]["frac_of_roofline_quantlinear_gemms"] = bound_us / gemm_us
+            out["cfg3_encoder"]["int8_peak_frac_attainable"] = gemm_ops / (bound_us * 1e-6) / PEAK_INT8_OPS
             # BASELINE configs 4 and 5 (secondary lines): int4 weights at B=32, and the
             # per-GPU shard of the 8-GPU config (B=2048 / 8 = 256 sentences)
             m4 = QtxModel(sd, ModelConfig(weight_bits=4))
