@@ -167,14 +167,14 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   }
   const float den = (t[0] + t[1]) + (t[2] + t[3]);
   // e/den correctly rounded via the shared reciprocal (div_cr) unless some e is outside
-  // its range (then the true division, wave-uniform); q/127 likewise (always in range)
+  // its range (then the true division, wave-uniform); q/127 by div127 (exact for the codes)
   DivRange rg;
 #pragma unroll
   for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
     for (int e = 0; e < 4; ++e) rg.add(x[kt][e]);
   const bool fast = __ballot(!(rg.ok() && divisor_ok(den))) == 0ull;
-  const float rden = 1.0f / den, r127 = 1.0f / 127.0f;
+  const float rden = 1.0f / den;
   if (fast) {
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt)
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {      // keys >= Sk: P = 0 (their padded PV steps add 0)
-      const float pq = div_cr(rintf(x[kt][e] * 127.0f), 127.0f, r127);
+      const float pq = div127(rintf(x[kt][e] * 127.0f));
       x[kt][e] = (16 * kt + 4 * e + fg < Sk) ? pq : 0.0f;
     }
   QTX_STAMP(3);
@@ -390,12 +390,12 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
     // P = rint((e / den) * 127) / 127 with both divisions by div_cr, unguarded: den is in
     // [1, 128] (the row max contributes qexp(0) == 1), so e / den is correctly rounded for
     // every e >= 2^-60, and e < 2^-60 (or 0) gives P == 0 through either quotient
-    const float rden = 1.0f / den, r127 = 1.0f / 127.0f;
+    const float rden = 1.0f / den;
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        x[kt][e] = div_cr(rintf(div_cr(x[kt][e], den, rden) * 127.0f), 127.0f, r127);
+        x[kt][e] = div127(rintf(div_cr(x[kt][e], den, rden) * 127.0f));
   };
   // ---- PV: A = P[row fr][k = 4 s4 + fg], B[k][n] = float(v[k][64h + 4n + dt]) * s_v[k] --
   // in chunks of 32 keys (the V operand reads of a chunk are issued ahead of its MFMAs);

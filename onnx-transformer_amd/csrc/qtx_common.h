@@ -237,6 +237,14 @@ __device__ __forceinline__ void div_const_n(float (&a)[R], float b) {
   }
 }
 
+// RN(c / 127) for an integer-valued c in [0, 127] (a P code, attention.py's P grid) in two
+// operations instead of div_cr's three or a true division: fma(c, RN(1/127), c * lo) with
+// lo = RN(1/127 - RN(1/127)) = RN(1/127) * 2^-28.  Checked for every c against the exactly
+// rounded quotient (rational arithmetic; tools/ and DESIGN.md §3).
+__device__ __forceinline__ float div127(float c) {
+  return fmaf(c, 0x1.020408p-7f, c * 0x1.020408p-35f);
+}
+
 // ---------------------------------------------------------------- quantizer
 // quant_linear.py:30-43 / :5-17:  s = max(absmax, 1e-5) / qmax;  q = rint(x / s).
 __device__ __forceinline__ float quant_scale(float absmax, float qmax) {

@@ -690,11 +690,15 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
       lsum = lsum + e;
     }
   }
+  // P = rint((e / den) * 127) / 127: e / den by div_cr, unguarded (den in [1, Sk]: the
+  // row max contributes qexp(0) == 1; e >= 2^-60 gives the correctly rounded quotient and
+  // e < 2^-60 a P of 0 through either), / 127 by div127 — no true division per key
   const float den = wave_sum(lsum);
+  const float rden = 1.0f / den;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int j = lane + 64 * u;
-    if (j < Sk) P[j] = rintf((P[j] / den) * 127.0f) / 127.0f;
+    if (j < Sk) P[j] = div127(rintf(div_cr(P[j], den, rden) * 127.0f));
   }
   __syncthreads();
   QTX_STAMP(2);
