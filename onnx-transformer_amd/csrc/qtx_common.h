@@ -55,6 +55,15 @@ static __device__ unsigned long long* qtx_stamp_buf;
 
 namespace qtx {
 
+// VM_CNT_ORDER.  On gfx950 (as on every GFX9 target) loads and stores share vmcnt, and a
+// store may retire before a load issued ahead of it; only loads retire in issue order
+// among themselves (LLVM's SIInsertWaitcnts treats a counter with both pending as out of
+// order).  So a hand-counted "s_waitcnt vmcnt(N)" that waits for an LDS-DMA is exact only
+// when the N newest operations are loads; with stores behind the DMA it must be vmcnt(0).
+// The weight-stationary kernels once counted the stores behind their DMA (vmcnt(3)): two
+// encodes on two streams then read blocks whose DMA had not landed (wrong whole sentences
+// in ~1 of 6 runs, tests/test_gpu_configs.py two_threads, tools/conc_encode_diag.py).
+
 // ---------------------------------------------------------------- wave reductions
 // Canonical sum of 64 lane values = the balanced pairwise tree over lanes in natural
 // order: ((l0+l1)+(l2+l3)) ... — what an xor-butterfly computes in every lane.
@@ -164,7 +173,9 @@ __device__ __forceinline__ float qexp(float x) {
   // double-rounding ambiguity between the two sides)
   const float xc = fmaxf(x, -100.0f);                  // keeps (int)n in range
   const float n = rintf(xc * 0x1.715476p+0f);          // log2(e)
-  float r = xc - n * 0x1.62e4p-1f;                      // ln2 hi
+  // ln2 hi has a 15-bit significand and |n| <= 145, so n * ln2hi is exact and the fma is
+  // bit-identical to the separate multiply and subtract (one VALU instead of two)
+  float r = fmaf(-n, 0x1.62e4p-1f, xc);                 // ln2 hi
   r = r - n * 0x1.7f7d1cp-20f;                         // ln2 lo
   float p = 0x1.a01a02p-13f;                           // 1/5040
   p = fmaf(p, r, 0x1.6c16c2p-10f);                     // 1/720

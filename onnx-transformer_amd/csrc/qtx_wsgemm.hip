@@ -124,13 +124,11 @@ __global__ __launch_bounds__(512) void k_gemm_ws(RowGemmArgs g) {
   for (int rb = r0; rb < nb; rb += wpt, ++it) {
     const int m0 = rb * WS_R;
     uint8_t* cur = lds + (NST == 2 ? (it & 1) * WS_STAGE : 0);
-    // this wave's DMA of the block retired (only the previous epilogue's unconditional
-    // stores, issued after it, may still be in flight: vmcnt retires in issue order); the
-    // barrier makes every wave's part visible and frees the other stage / the epilogue areas
-    if constexpr (EPI == RE_QUANT) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else if constexpr (EPI == RE_RELU_QUANT_PMAX) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if constexpr (EPI == RE_RELU_PMAX) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's DMA of the block retired, and with it the previous epilogue's stores:
+    // VM_CNT_ORDER (qtx_common.h) — a store issued after the DMA may retire before it, so a
+    // count that leaves the stores in flight could release the barrier early; the barrier
+    // makes every wave's part visible and frees the other stage / the epilogue areas
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (it == 0) QTX_STAMP(1);
@@ -607,12 +605,11 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
     }
   };
   auto top_wait = [&]() {
-    // the block's DMA retired (only the previous epilogue's stores — 3 per wave for the
-    // quantizing epilogues (2 rows of 16 bytes + the scale), 1 for RELU_PMAX — may still
-    // fly), then every wave's part visible (compiler-visible waits: its own wait insertion
-    // then knows what they retired)
-    if constexpr (EPI == RE_RELU_PMAX) __builtin_amdgcn_s_waitcnt(WAIT_VM(1));
-    else __builtin_amdgcn_s_waitcnt(WAIT_VM(3));
+    // the block's DMA retired, and the previous epilogue's stores with it (VM_CNT_ORDER,
+    // qtx_common.h: stores issued after the DMA may retire before it), then every wave's
+    // part visible (compiler-visible waits: its own wait insertion then knows what they
+    // retired)
+    __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
     __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
     __builtin_amdgcn_s_barrier();
   };
@@ -843,8 +840,9 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   const __amdgpu_buffer_rsrc_t srsrc = ws_rsrc(g.os + (long)t * g.os_ts, 4L * g.M);
   auto redb = [&](int k) { return red0 + (k & 1) * 8 * WP_R; };
   auto top_wait = [&]() {
-    // the block's DMA retired (behind it only the previous iteration's 3 stores per wave)
-    __builtin_amdgcn_s_waitcnt(WAIT_VM(3));
+    // the block's DMA retired, and the previous iteration's 3 stores per wave with it
+    // (VM_CNT_ORDER, qtx_common.h: a count leaving them in flight can release early)
+    __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
     __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
     __builtin_amdgcn_s_barrier();
   };
@@ -1098,7 +1096,7 @@ __global__ __launch_bounds__(512) void k_gemm_wss(RowGemmArgs g) {
     for (int i = 0; i < 2; ++i) sr[i] = sal[((k & 1) * 8 + wave) * 64 + 16 * i + f];
   };
   auto top_wait = [&]() {
-    __builtin_amdgcn_s_waitcnt(WAIT_VM(3));      // behind the block's DMA: 3 stores per wave
+    __builtin_amdgcn_s_waitcnt(WAIT_VM(0));      // the block's DMA and the stores after it (VM_CNT_ORDER)
     __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
     __builtin_amdgcn_s_barrier();
   };
@@ -1496,10 +1494,10 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
   // ---- steady state: iteration k: MFMAs of block k, y + maxima of block k-1 (published),
   // quantization of block k-2
   for (int k = 1; k <= nblk; ++k) {
-    // block k's DMA retired (behind it only the previous iteration's stores: 3 per wave —
-    // iteration 1, which quantizes nothing, issues 3 dropped ones — plus wave 0's granule
-    // store: vmcnt(3) over-waits on wave 0, never under-waits)
-    __builtin_amdgcn_s_waitcnt(WAIT_VM(3));
+    // block k's DMA retired, and the previous iteration's stores (3 per wave, plus wave 0's
+    // granule store) with it: VM_CNT_ORDER (qtx_common.h) — a store issued after the DMA
+    // may retire before it, so vmcnt(3) could release the barrier with the DMA in flight
+    __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
     __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
     __builtin_amdgcn_s_barrier();
     const bool more = k < nblk;     // block k exists (uniform)
@@ -1556,10 +1554,9 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
 // a whole iteration as in k_gemm_wsx.  The exchange (tickets, granules, bounded waits that
 // report DEV_E_EXCHANGE_TIMEOUT) is k_gemm_wsx's.  Numerics as k_gemm_wsq: RN(y / s) by
 // div_cr with the row's reciprocal, s by true division.
-// Wait ordering: vmcnt counts loads and stores in order, so the granule loads (which are
-// waited for at once) go before this iteration's DMA and stores, behind only the previous
-// iteration's stores; every iteration issues 3 stores after its DMA (dropped ones where
-// there is nothing to store) for the vmcnt(3) at the next top.
+// Wait ordering: the granule loads (waited for at once) go before this iteration's DMA and
+// stores; the top of an iteration waits vmcnt(0) (VM_CNT_ORDER, qtx_common.h: a store may
+// retire before a DMA issued ahead of it, so counting the stores behind the DMA is unsafe).
 // =====================================================================================
 template <int PRIO = 0, int LAG = 1>   // as k_gemm_wsq
 __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
@@ -1795,7 +1792,7 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
   auto iter = [&](int k, float (&yb)[2][16], float& mb, float& mo) {
     const long long t0 = QTX_NOW();
     if (k > 0) {
-      __builtin_amdgcn_s_waitcnt(WAIT_VM(3));   // block k's DMA retired (behind: 3 stores)
+      __builtin_amdgcn_s_waitcnt(WAIT_VM(0));   // block k's DMA and the 3 stores after it (VM_CNT_ORDER)
       __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
       __builtin_amdgcn_s_barrier();
     }
@@ -1921,8 +1918,9 @@ __global__ __launch_bounds__(512) void k_gemm_wsr(RowGemmArgs g) {
   __builtin_amdgcn_s_barrier();
   for (int k = 0; k < nblk; ++k) {
     if (k > 0) {
-      // block k's DMA retired: behind it only block k-1's 20 stores (4 rounds x 5)
-      __builtin_amdgcn_s_waitcnt(WAIT_VM(20));
+      // block k's DMA retired, and block k-1's 20 stores (4 rounds x 5) with it
+      // (VM_CNT_ORDER, qtx_common.h)
+      __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
       __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
       __builtin_amdgcn_s_barrier();
     }

@@ -97,6 +97,13 @@ def test_cfg3_encoder_split_two_threads(torch, gpu_model, cfg3_inputs, cfg3_spli
     x, m = cfg3_inputs
     x2 = np.ascontiguousarray(x[::-1])      # a different batch: the sentences reversed
     m2 = np.ascontiguousarray(m[::-1])
+    # several rounds: the race this guards against (a counted vmcnt releasing a block before
+    # its DMA landed, qtx_common.h VM_CNT_ORDER) showed in about one round of six
+    for _ in range(4):
+        _two_threads_round(torch, gpu_model, x, m, x2, m2, cfg3_split)
+
+
+def _two_threads_round(torch, gpu_model, x, m, x2, m2, cfg3_split):
     res, errs = {}, []
 
     def run(tag, xx, mm):
