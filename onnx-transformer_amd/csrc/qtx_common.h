@@ -299,22 +299,25 @@ __device__ __forceinline__ uint32_t pack4_biased(float t0, float t1, float t2, f
 template <int N>
 __device__ __forceinline__ void quant_pack(const float* x, float s, uint32_t* out) {
   static_assert(N % 4 == 0, "groups of 4");
+  // the tie test on the biased rint the packing needs anyway (as quant_rows512):
+  // t = RN(r + 1.5 * 2^23), |r - (t - 1.5 * 2^23)| > 0.5 - 2^-13 is exactly
+  // |frac(r) - 0.5| < 2^-13, folded with one max per value
+  constexpr float BIAS = 12582912.0f;
   const float inv = __builtin_amdgcn_rcpf(s);
-  float r[N];
-  bool near = false;
+  float t[N];
+  float dm = 0.0f;
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    r[i] = x[i] * inv;
-    near |= fabsf((r[i] - floorf(r[i])) - 0.5f) < 0x1p-13f;
+    const float r = x[i] * inv;
+    t[i] = r + BIAS;
+    dm = fmaxf(dm, fabsf(r - (t[i] - BIAS)));
   }
-  if (__builtin_expect(__ballot(near) != 0ull, 0)) {
+  if (__builtin_expect(__ballot(dm > 0.5f - 0x1p-13f) != 0ull, 0)) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) r[i] = x[i] / s;
+    for (int i = 0; i < N; ++i) t[i] = x[i] / s + BIAS;
   }
 #pragma unroll
-  for (int i = 0; i < N / 4; ++i)
-    out[i] = pack4_biased(rint_biased(r[4 * i]), rint_biased(r[4 * i + 1]),
-                          rint_biased(r[4 * i + 2]), rint_biased(r[4 * i + 3]));
+  for (int i = 0; i < N / 4; ++i) out[i] = pack4_biased(t[4 * i], t[4 * i + 1], t[4 * i + 2], t[4 * i + 3]);
 }
 // single value per lane
 __device__ __forceinline__ int quant_one(float x, float s) {
