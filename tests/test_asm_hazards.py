@@ -26,3 +26,17 @@ def test_asm_mfma_wait_states(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:]
     for k in ("k_gemm_wsq", "k_gemm_wss", "k_gemm_wsy"):
         assert f"{k}: 0 hazards" in r.stdout, r.stdout[-2000:]
+
+
+def test_ws_kernels_wait_vmcnt_zero():
+    """VM_CNT_ORDER (csrc/qtx_common.h): the weight-stationary kernels store inside their
+    block loops, and a store may retire before an LDS-DMA issued ahead of it, so their
+    hand-written waits must be vmcnt(0) — a count that leaves stores in flight can release
+    a barrier before the block's DMA landed (the race fixed in round 3)."""
+    import os
+    import re
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "onnx-transformer_amd", "csrc", "qtx_wsgemm.hip")).read()
+    code = "\n".join(l.split("//")[0] for l in src.splitlines())
+    assert not re.search(r"WAIT_VM\(\s*[1-9]", code), "counted WAIT_VM in a ws kernel"
+    assert not re.search(r"vmcnt\(\s*[1-9]", code), "counted vmcnt in a ws kernel"
