@@ -311,6 +311,27 @@ def time_row_gemms(M=256 * 128, reps=10, ws=True, operands="encoder"):
     return res
 
 
+def time_encoder_cfg3(model=None, B=256, S=128, n=5):
+    """Seconds per encoder-only forward at B x S (BASELINE cfg3), HIP events."""
+    import torch
+    if model is None:
+        from qtx.model import QtxModel
+        from qtx.weights import synthetic_state_dict
+        model = QtxModel(synthetic_state_dict(20241223))
+    xs = torch.randn((B, S, D), device="cuda")
+    mk = torch.ones((B, S), dtype=torch.uint8, device="cuda")
+    for _ in range(2):
+        model.encode(xs, mk)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        model.encode(xs, mk)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / n
+
+
 def time_decode(model, B, S, L, steps=3, seed=1000):
     """ms per greedy decode (encoder + L-1 steps) of B synthetic sentences."""
     import torch
@@ -537,19 +558,7 @@ def main():
                "roofline": roof, "step": step}
         if not args.no_cfg3:
             Bc, Sc = 256, 128
-            xs = torch.randn((Bc, Sc, D), device="cuda")
-            mk = torch.ones((Bc, Sc), dtype=torch.uint8, device="cuda")
-            for _ in range(2):
-                model.encode(xs, mk)
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            n = 5
-            for _ in range(n):
-                model.encode(xs, mk)
-            e1.record()
-            torch.cuda.synchronize()
-            te = e0.elapsed_time(e1) / 1e3 / n
+            te = time_encoder_cfg3(model, Bc, Sc)
             ops = encoder_gemm_ops(Bc, Sc)
             g = time_row_gemms(Bc * Sc)
             gemm_us = sum(t for t, _ in g.values())
