@@ -293,6 +293,10 @@ def time_row_gemms(M=256 * 128, reps=10, ws=True, operands="encoder"):
              # is the exchange scratch), as the encoder runs it
              ("ffn1_quant_onepass", F, D, a512, dict(epi=3, kp=3, pmax_out=gx, out8=out8, ldo8=F, os=os_)),
              ("ffn2_res_ln", D, F, a2048, dict(epi=1, res=x, xout=x, ln_a=lna, ln_b=lnb, lnq=out8, lns=os_))]
+    if os.environ.get("QTX_BENCH_FFN1_2PASS", "0") == "1":
+        # FFN1 as two weight-stationary passes (row maxima, then ReLU + quant from them)
+        cases[2:3] = [("ffn1_rowmax", F, D, a512, dict(epi=2, pmax_out=pm)),
+                      ("ffn1_quant", F, D, a512, dict(epi=3, pmax_in=pm, pmax_n=4, out8=out8, ldo8=F, os=os_))]
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     res = {}
     for name, N, K, a, kw in cases:

@@ -1697,6 +1697,8 @@ int32_t qtx_linear_rows(const qtx_row_gemm* a, void* stream) {
   if (g.ksplit > 1 && (g.epi != RE_RES_LN || g.kp != 1 || !g.part || (g.ksplit & (g.ksplit - 1)) ||
                        g.ksplit > 8))
     return fail(QTX_E_INVALID, "ksplit %d: epi 1 with kp 1, a power of two <= 8, and part", g.ksplit);
+  if (g.ksplit > 1 && (g.K % 64 || (g.K / 64) % (4 * g.ksplit)))   // launch_gemm_row's split
+    return fail(QTX_E_INVALID, "ksplit %d needs K / 64 a multiple of 4 * ksplit (K=%d)", g.ksplit, g.K);
   const bool ok = (g.epi == RE_QUANT && g.out8 && g.os) ||
                   (g.epi == RE_RES_LN && g.res && g.xout && g.ln_a && g.ln_b &&
                    (g.lnq ? g.lns != nullptr : g.lnout != nullptr)) ||

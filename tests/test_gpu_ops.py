@@ -398,7 +398,10 @@ def test_linear_rows_kp(torch, oracle_model, M):
 
 
 @pytest.mark.parametrize("M,wsq", [(300, 1), (7, 1), (20011, 1), (4096, 1), (4096, 0),
-                                   (300, 2), (7, 2), (20011, 2), (4096, 2), (64, 2)])
+                                   (300, 2), (7, 2), (20011, 2), (4096, 2), (64, 2),
+                                   (300, 3), (7, 3), (20011, 3), (4096, 3), (8160, 3), (32768, 3),
+                                   (64, 3), (300, 4), (7, 4), (20011, 4), (4096, 4), (8160, 4),
+                                   (32768, 4), (64, 4), (2720, 4), (4080, 4), (5440, 4)])
 def test_linear_rows_ws_qkv_scales(torch, M, wsq, monkeypatch):
     """Q/K/V (epi 0, kp = 2) on the weight-stationary kernels (QTX_WSQ=1: k_gemm_wsq, the
     default, one barrier per block, quantization interleaved between the MFMAs; 0:
@@ -456,6 +459,34 @@ def test_linear_rows_ws_ffn1_onepass_scales(torch, M, wsy, monkeypatch):
     assert status == 0
 
 
+@pytest.mark.parametrize("M", [7, 300, 4096, 20011, 32768, 2720, 64])
+def test_linear_rows_ws_ffn1_twopass_wsa2(torch, M, monkeypatch):
+    """FFN1 as two weight-stationary passes on k_gemm_wsa2 (QTX_WSA2=1: one wave per SIMD,
+    W1's slice in AGPRs): the row-max pass (epi 2 -> 4 slice maxima per row), then the
+    ReLU + per-token quantization pass (epi 3, pmax_in); row scales 1e-35 .. 1e25, bit-exact."""
+    from qtx._lib import lib
+    monkeypatch.setenv("QTX_WSA2", "1")
+    rng = np.random.default_rng(M + 57)
+    qx, sx = O.quant_rows(rng.standard_normal((M, 512)).astype(f32))
+    sx = (sx * np.float32(10.0) ** rng.integers(-33, 26, M)).astype(f32)
+    qw, sw = O.quant_weight((rng.standard_normal((2048, 512)) * 0.05).astype(f32), 8)
+    b = (rng.standard_normal(2048) * 1e-3).astype(f32)
+    wk = torch.empty((2048, 512), dtype=torch.int8, device="cuda")
+    assert lib().qtx_pack_w_ws(P(dev(torch, qw)), 2048, 512, P(wk), S0) == 0
+    h8 = torch.zeros((M + (M & 1), 2048), dtype=torch.int8, device="cuda")
+    sh = torch.full((M,), -1.0, dtype=torch.float32, device="cuda")
+    pm = torch.full((4, M), -1.0, dtype=torch.float32, device="cuda")
+    base = dict(A=dev(torch, _to_kp(qx)), sa=dev(torch, sx), W=wk, sw=dev(torch, sw),
+                bias=dev(torch, b), M=M, N=2048, K=512, kp=2)
+    _rows_call(torch, **base, epi=2, pmax_out=pm)
+    h = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b, relu=True)
+    np.testing.assert_array_equal(pm.cpu().numpy(), np.abs(h).reshape(M, 4, 512).max(-1).T)
+    _rows_call(torch, **base, epi=3, pmax_in=pm, pmax_n=4, out8=h8, ldo8=2048, os=sh)
+    qh, s = O.quant_rows(h)
+    np.testing.assert_array_equal(_from_kp(h8.cpu().numpy(), M), qh)
+    np.testing.assert_array_equal(sh.cpu().numpy(), s)
+
+
 @pytest.mark.parametrize("M,ks,lnq", [(7, 4, True), (300, 4, True), (2304, 4, True),
                                       (300, 2, True), (300, 8, True), (129, 4, False),
                                       (8192, 4, True)])
@@ -490,6 +521,23 @@ def test_linear_rows_res_ln_splitk(torch, oracle_model, M, ks, lnq):
         np.testing.assert_array_equal(out["lns"].cpu().numpy(), s2)
     else:
         np.testing.assert_array_equal(out["lnout"].cpu().numpy(), ln)
+
+
+def test_linear_rows_splitk_bad_k_is_invalid(torch):
+    """A split-K shape the launcher cannot tile (K / 64 not a multiple of 4 * ksplit) is an
+    argument error (QTX_E_INVALID = 1 at the C-ABI), not a HIP error."""
+    from qtx._lib import RowGemm, lib
+    import ctypes as C
+    M = 64
+    z8 = torch.zeros((M, 512), dtype=torch.int8, device="cuda")
+    f = torch.zeros(M * 512, dtype=torch.float32, device="cuda")
+    a = RowGemm()
+    kw = dict(A=z8, sa=f, W=z8, sw=f, bias=f, M=M, N=512, K=512, epi=1, res=f, xout=f,
+              ln_a=f, ln_b=f, lnq=z8, lns=f, kp=1, part=f, ksplit=4)
+    for k, v in kw.items():
+        setattr(a, k, v.data_ptr() if hasattr(v, "data_ptr") else v)
+    assert lib().qtx_linear_rows(C.byref(a), S0) == 1
+    assert b"ksplit" in lib().qtx_last_error()
 
 
 def _ws_pack_ref(w):
