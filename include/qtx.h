@@ -338,6 +338,13 @@ int32_t qtx_decode_argmax_embed(const qtx_model* m, const float* logits, int32_t
  * counterpart). */
 int32_t qtx_debug_nop(void* stream);
 
+/* Re-read the library's environment switches (csrc/qtx_knobs.h), which are otherwise read
+ * once: the path switches the tests use to force the library's alternative code paths
+ * (QTX_NO_GRAPH, QTX_UNFUSED, QTX_DECODE_GROUPS, QTX_NO_WSX, ...) and the hooks of the FFN1
+ * exchange's error path (QTX_WSX_SPIN_LIMIT, QTX_WSX_DROP_SLICE).  Not for concurrent use
+ * with running calls (test / measurement only, no reference counterpart). */
+int32_t qtx_debug_reload_knobs(void);
+
 #ifdef __cplusplus
 }
 #endif

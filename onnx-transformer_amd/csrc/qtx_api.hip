@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -15,6 +16,7 @@
 
 #include "../../include/qtx.h"
 #include "qtx_kernels.h"
+#include "qtx_knobs.h"
 
 using namespace qtx;
 
@@ -120,12 +122,7 @@ struct qtx_model {
   hipStream_t estream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_lag = nullptr, ev_join = nullptr;
   int device = 0;            // the device the model's memory lives on
-  // device status word (DEV_E_* bits OR-ed by kernels that detect an error they cannot
-  // repair: k_gemm_wsx's exchange timeout) and its pinned host mirror, copied at the end
-  // of every model-level call and checked at the start of the next one (qtx_model_check:
-  // at once, after synchronising the caller's stream)
-  unsigned* status_dev = nullptr;
-  unsigned* status_host = nullptr;
+  unsigned long long serial = 0;   // unique per created model (call status records)
   // an exec may still be running on a caller's stream: wait for its last replay first
   void clear_graphs() {
     for (auto& kv : graphs) {
@@ -163,17 +160,33 @@ const char* status_text(unsigned v) {
                "FFN hidden was quantized from a partial row maximum): outputs invalid"
              : "device status word set";
 }
-// at the start of a model-level call: an error an earlier call on this model left behind
-// (its mirror landed) is reported now, and cleared
-int status_pending(const qtx_model* m, hipStream_t st) {
-  const unsigned v = __atomic_exchange_n(m->status_host, 0u, __ATOMIC_ACQ_REL);
-  if (!v) return QTX_OK;
-  HIPCHK(hipMemsetAsync(m->status_dev, 0, sizeof(unsigned), st));
-  return fail(QTX_E_DEVICE, "%s (reported by a previous call on this model)", status_text(v));
-}
-// at the end of a model-level call: the mirror of the word follows the call's kernels
-int status_publish(const qtx_model* m, hipStream_t st) {
-  HIPCHK(hipMemcpyAsync(m->status_host, m->status_dev, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+// Every model-level call has its OWN status word: the first 256 bytes of its workspace
+// (the caller's memory: one workspace per calling thread, include/qtx.h).  The call zeroes
+// it on its stream before its kernels run; a kernel that detects an error it cannot repair
+// (k_gemm_wsy's exchange timeout) ORs a DEV_E_* bit into it.  qtx_model_check(m, stream)
+// synchronises the stream and reads the word of the calling thread's last call on m, so an
+// error is reported to the thread whose call raised it and no other thread's call can clear
+// it (one word per model let another thread's check wipe it).
+struct CallStatus {
+  const qtx_model* m = nullptr;
+  unsigned long long serial = 0;    // the model's creation serial (a new model at a freed
+  unsigned* word = nullptr;         // address is a different model)
+};
+constexpr int kCallSlots = 8;
+thread_local CallStatus t_calls[kCallSlots];
+thread_local int t_next = 0;
+
+unsigned* take_call_status(Arena& ar) { return ar.take<unsigned>(64); }
+
+int call_status_begin(const qtx_model* m, unsigned* word, hipStream_t st) {
+  HIPCHK(launch_zero(word, sizeof(unsigned), st));     // a kernel: graph-capturable, ordered
+  for (CallStatus& c : t_calls)
+    if (c.m == m && c.serial == m->serial) {
+      c.word = word;
+      return QTX_OK;
+    }
+  t_calls[t_next] = CallStatus{m, m->serial, word};
+  t_next = (t_next + 1) % kCallSlots;
   return QTX_OK;
 }
 
@@ -280,10 +293,11 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     float* gb = ar.take<float>(c.tgt_vocab);
     int8_t* tmp = ar.take<int8_t>((size_t)F * D);
     m->gen_wt = ar.take<float>((size_t)((c.tgt_vocab + 15) / 16) * 16 * D);
-    m->status_dev = ar.take<unsigned>(64);
     return std::make_tuple(norms, src_lut, tgt_lut, pe_d, gw, gb, tmp);
   };
   qtx_model* m = new qtx_model();
+  static std::atomic<unsigned long long> next_serial{1};
+  m->serial = next_serial.fetch_add(1);
   m->cfg = c;
   (void)hipGetDevice(&m->device);
   Arena sizing;
@@ -365,10 +379,6 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
   m->src_lut = src_lut; m->tgt_lut = tgt_lut; m->pe = pe_d; m->gen_w = gw; m->gen_b = gb;
   he = launch_pack_gen(gw, c.tgt_vocab, m->gen_wt, st);
   if (he != hipSuccess) { qtx_model_destroy(m); return fail(QTX_E_HIP, "pack generator"); }
-  he = hipMemsetAsync(m->status_dev, 0, sizeof(unsigned), st);
-  if (he == hipSuccess) he = hipHostMalloc(reinterpret_cast<void**>(&m->status_host), sizeof(unsigned));
-  if (he != hipSuccess) { qtx_model_destroy(m); return fail(QTX_E_HIP, "status word"); }
-  *m->status_host = 0u;
   he = hipStreamSynchronize(st);
   if (he != hipSuccess) {
     qtx_model_destroy(m);
@@ -392,7 +402,6 @@ int32_t qtx_model_destroy(qtx_model* m) {
     if (m->gstream[i]) (void)hipStreamDestroy(m->gstream[i]);
   }
   if (m->mem) (void)hipFree(m->mem);
-  if (m->status_host) (void)hipHostFree(m->status_host);
   delete m;
   return QTX_OK;
 }
@@ -484,6 +493,7 @@ struct Scratch {
   int8_t* h8;    // [M, F]  quantized FFN hidden
   float* sh;     // [M]
   float* pmax;   // [F/512, M] FFN1 per-tile row maxima
+  unsigned* status = nullptr;   // the call's status word (call_status_begin)
 };
 
 Scratch carve_scratch(Arena& ar, const qtx_config& c, long M) {
@@ -550,7 +560,7 @@ int linear(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa
 
 // Row-complete GEMM (k_gemm_row) for 8-bit weights: epilogues of whole 512-wide rows.
 bool row_path(const qtx_config& c) {   // (4-bit models: on the unpacked int8 weights)
-  return c.d_ff % 512 == 0 && !getenv("QTX_NO_ROWGEMM");
+  return c.d_ff % 512 == 0 && !knobs().no_rowgemm;
 }
 // kp: A (a8) in the KP layout and W from L.qkp; the int8 lnq / FFN-hidden outputs are
 // then written KP as well (RE_QUANT's q8 stays row-major: attention reads it).
@@ -562,18 +572,8 @@ bool row_path(const qtx_config& c) {   // (4-bit models: on the unpacked int8 we
 // 0.73 ms (the row GEMM's 128-row tiles give 18 workgroups).  The O-projection's residual +
 // LayerNorm epilogue runs weight-stationary only between ws_res_min_m and ws_res_max_m
 // (above it the KP row GEMM is faster).  QTX_WS_MIN_M / QTX_WS_RES_MIN_M / _MAX_M: A/B.
-long env_long(const char* name, long def) {
-  const char* e = getenv(name);
-  return e && *e ? atol(e) : def;
-}
-long ws_min_m() {
-  static const long v = env_long("QTX_WS_MIN_M", 2048L);
-  return v;
-}
-bool ws_res_ok(long M) {
-  static const long lo = env_long("QTX_WS_RES_MIN_M", 2048L), hi = env_long("QTX_WS_RES_MAX_M", 8192L);
-  return M >= lo && M < hi;
-}
+long ws_min_m() { return knobs().ws_min_m; }
+bool ws_res_ok(long M) { return M >= knobs().ws_res_min_m && M < knobs().ws_res_max_m; }
 RowGemmArgs rowgemm(const QLin& L, const int8_t* a8, const float* sa, int M, int epi,
                     bool kp = false) {
   RowGemmArgs g{};
@@ -608,7 +608,7 @@ int row_res_ln(const QLin& L, const int8_t* a8, const float* sa, int M, float* x
   g.res = x; g.xout = x; g.ln_a = ln[0]; g.ln_b = ln[1];
   g.lnq = lnq; g.lns = lns; g.lnout = lnout;
   if (part && g.kp == 1 && fa.kind == FK_NONE && (M + 127) / 128 <= 64 && L.K % 2048 == 0 &&
-      !getenv("QTX_NO_SPLITK")) {
+      !knobs().no_splitk) {
     g.part = reinterpret_cast<int32_t*>(part);
     g.ksplit = 4;
   }
@@ -619,13 +619,7 @@ int row_res_ln(const QLin& L, const int8_t* a8, const float* sa, int M, float* x
 // maxima, then recompute + quantize: cheaper than the fp32 hidden's round trip)
 // FFN1 in one weight-stationary pass with the row maxima exchanged between the column
 // slices' workgroups inside the launch (k_gemm_wsx); QTX_NO_WSX=1: the two passes
-bool wsx_on() {
-  static const bool v = [] {
-    const char* e = getenv("QTX_NO_WSX");
-    return !(e && *e && *e != '0');
-  }();
-  return v;
-}
+bool wsx_on() { return !knobs().no_wsx; }
 int row_ffn1(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa, int M,
              Scratch& s, hipStream_t st,
              const FaultArgs& fa = FaultArgs{}, bool kp = false, unsigned* status = nullptr) {
@@ -862,7 +856,7 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
   // (qtx_common.h kp_off); the fault variants keep the row-major layout.
   const int NL = c.n_layers;
   const bool kp = (f == nullptr || f->kind == QTX_FAULT_NONE) && m->enc[0].qkv.qkp &&
-                  !getenv("QTX_NO_KP");
+                  !knobs().no_kp;
   RC(ln_quant(s.x, M, m->enc[0].ln[0], D, s.a8, s.sa, st, kp));
   for (int l = 0; l < NL; ++l) {
     const EncLayer& L = m->enc[l];
@@ -875,7 +869,7 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
     AttnFault af;
     const hipError_t ea = attn_fault_for(f, 0, l, false, S, S, af)
                               ? hipErrorNotSupported
-                              : (getenv("QTX_NO_ATTN_ENCQ") ? hipErrorNotSupported
+                              : (knobs().no_attn_encq ? hipErrorNotSupported
                                                             : launch_attention_encq(a, s.a8, s.sa, st,
                                                                                     false, kp));
     if (attn_fault_for(f, 0, l, false, S, S, af)) {
@@ -887,7 +881,7 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
       HIPCHK(ea);
     }
     RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st, fa(G_O), kp));
-    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1), kp, m->status_dev));
+    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1), kp, s.status));
     if (l + 1 < NL)
       RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc[l + 1].ln[0], s.a8, s.sa, nullptr, st,
                     fa(G_FFN2), kp, s.y));
@@ -905,13 +899,15 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
 // (not with the one-pass FFN1, which makes the layer's kernels MFMA / exchange-bound rather
 // than HBM-bound: the split measured no gain before it, 2.07 vs 2.05 ms)
 bool wsx_on();
-bool enc_split(int B) { return B >= 256 && !getenv("QTX_ENC_NOSPLIT") && !wsx_on(); }
+bool enc_split(int B) { return B >= 256 && !knobs().enc_nosplit && !wsx_on(); }
 
 size_t enc_ws(const qtx_config& c, int B, int S) {
   Arena ar;
+  take_call_status(ar);
   carve_scratch(ar, c, (long)B * S);
   if (enc_split(B)) {
     Arena a2;
+    take_call_status(a2);
     carve_scratch(a2, c, (long)(B / 2) * S);
     carve_scratch(a2, c, (long)(B - B / 2) * S);
     ar.used = std::max(ar.used, a2.used);
@@ -1021,8 +1017,7 @@ struct Groups {
 };
 Groups decode_groups(int B) {
   int G = B >= 512 ? 2 : 1;
-  if (const char* v = getenv("QTX_DECODE_GROUPS"))
-    if (*v) G = atoi(v);
+  if (knobs().decode_groups > 0) G = knobs().decode_groups;
   G = std::max(1, std::min(std::min(G, QTX_MAX_GROUPS), B));
   const int Bg = (B + G - 1) / G;
   return Groups{(B + Bg - 1) / Bg, Bg};   // no empty group
@@ -1074,7 +1069,6 @@ GreedyWS group_view(const GreedyWS& g, const qtx_config& c, int i, int b0, int S
   return v;
 }
 
-bool env_flag(const char* name);
 
 // ---- fused decode step (M = B rows, keys <= 128) ----------------------------------------
 SkinnyArgs skinny(int wbits, const QLin& L, int M, int amode, int flags, float* out, long ldo) {
@@ -1094,16 +1088,15 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
                       int64_t* ids, const uint8_t* src_mask, hipStream_t st) {
   const qtx_config& c = m->cfg;
   const int D = c.d_model, F = c.d_ff, wb = m->dec[0].qkv.q8 ? 8 : c.weight_bits;
-  const bool ffn_qkernel = env_flag("QTX_FFN_QKERNEL");
-  const bool fused_ln = !env_flag("QTX_SPLIT_LN");
+  const bool ffn_qkernel = knobs().ffn_qkernel;
+  const bool fused_ln = !knobs().split_ln;
   Scratch& s = g.dec;
   // Timing experiments only (wrong results): QTX_ABLATE=<bitmask> drops kernel classes
   // from the step (replaced by an empty kernel with QTX_ABLATE_NOP=1) to measure what
   // each costs inside the real graph.  1 LN, 2 QKV/Qc, 4 self-attn, 8 cross-attn,
   // 16 O/Oc, 32 FFN1, 64 h-quant, 128 FFN2, 256 tail.
-  const char* abl_env = getenv("QTX_ABLATE");
-  const int abl = abl_env ? (int)strtol(abl_env, nullptr, 0) : 0;
-  const bool abl_nop = env_flag("QTX_ABLATE_NOP");
+  const int abl = knobs().ablate;           // always 0 outside the QTX_DIAG build
+  const bool abl_nop = knobs().ablate_nop;
 #define QTX_RUN(bit, launch)                   \
   do {                                         \
     if (abl & (bit)) {                         \
@@ -1171,7 +1164,7 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
       QTX_RUN(128, launch_skinny(a, wb, st));
     }
   }
-  if (getenv("QTX_DBG_TAIL")) {   // bisection aid: reference-shaped tail kernels
+  if (knobs().dbg_tail) {   // bisection aid (QTX_DIAG build): reference-shaped tail kernels
     RC(ln_out(s.x, B, m->dec_norm, D, g.xo, st));
     HIPCHK(launch_generator(g.xo, D, B, m->gen_w, m->gen_b, c.tgt_vocab, g.logits, st));
     HIPCHK(launch_logsoftmax_argmax(g.logits, B, c.tgt_vocab, nullptr, ids, max_len, g.step,
@@ -1227,10 +1220,6 @@ int greedy_step_unfused(const qtx_model* m, GreedyWS& g, int B, int S, int max_l
   return QTX_OK;
 }
 
-bool env_flag(const char* name) {
-  const char* v = getenv(name);
-  return v && *v && strcmp(v, "0") != 0;
-}
 
 int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S, int max_len,
                int64_t start, const qtx_fault* f, hipStream_t st);
@@ -1248,6 +1237,7 @@ size_t qtx_decoder_workspace_size(const qtx_model* m, int32_t B, int32_t T, int3
 size_t qtx_greedy_workspace_size(const qtx_model* m, int32_t B, int32_t S, int32_t max_len) {
   if (!m) return 0;
   Arena ar;
+  take_call_status(ar);
   carve_greedy(ar, m->cfg, B, S, max_len);
   return align_up(ar.used);
 }
@@ -1262,11 +1252,12 @@ int32_t qtx_encoder_forward_fault(const qtx_model* m, const float* x, const uint
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
   hipStream_t st = (hipStream_t)stream;
-  RC(status_pending(m, st));
+  unsigned* cst = take_call_status(ar);
+  RC(call_status_begin(m, cst, st));
   if (!enc_split(B) || (f && f->kind != QTX_FAULT_NONE)) {
     Scratch s = carve_scratch(ar, m->cfg, (long)B * S);
-    RC(encoder_run(m, x, src_mask, B, S, out, s, st, f));
-    return status_publish(m, st);
+    s.status = cst;
+    return encoder_run(m, x, src_mask, B, S, out, s, st, f);
   }
   // The model's second stream and its three events are shared by every caller: the lock
   // is held across the whole record / wait sequence, so two threads' fork, lag and join
@@ -1284,6 +1275,7 @@ int32_t qtx_encoder_forward_fault(const qtx_model* m, const float* x, const uint
   const long D = m->cfg.d_model;
   Scratch s0 = carve_scratch(ar, m->cfg, (long)B0 * S);
   Scratch s1 = carve_scratch(ar, m->cfg, (long)B1 * S);
+  s0.status = s1.status = cst;
   // half 1 starts when half 0's first layer has passed its QKV GEMM (ev_lag)
   HIPCHK(hipEventRecord(mm->ev_fork, st));
   HIPCHK(hipStreamWaitEvent(mm->estream, mm->ev_fork, 0));
@@ -1293,7 +1285,7 @@ int32_t qtx_encoder_forward_fault(const qtx_model* m, const float* x, const uint
                  s1, mm->estream, nullptr));
   HIPCHK(hipEventRecord(mm->ev_join, mm->estream));
   HIPCHK(hipStreamWaitEvent(st, mm->ev_join, 0));
-  return status_publish(m, st);
+  return QTX_OK;
 }
 
 int32_t qtx_encoder_forward(const qtx_model* m, const float* x, const uint8_t* src_mask,
@@ -1348,7 +1340,7 @@ int32_t qtx_decoder_forward_fault(const qtx_model* m, const float* y, const floa
     if (attn_fault_for(f, 1, l, false, T, T, af)) {
       RC(attention_fault(a, af, M, D, s, st));
     } else {
-      const hipError_t ea = getenv("QTX_NO_ATTN_ENCQ") ? hipErrorNotSupported
+      const hipError_t ea = knobs().no_attn_encq ? hipErrorNotSupported
                                                        : launch_attention_encq(a, s.a8, s.sa, st);
       if (ea == hipErrorNotSupported) {  // other shapes: fp32 context + quantization kernel
         HIPCHK(launch_attention(a, st));
@@ -1427,17 +1419,19 @@ int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
                                    "qtx_decoder_forward_fault on the step's prefix)");
   RC(check_fault(m, f, 0, B, S, 0));
   hipStream_t st = (hipStream_t)stream;
-  RC(status_pending(m, st));
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
+  unsigned* cst = take_call_status(ar);
+  RC(call_status_begin(m, cst, st));
   GreedyWS g = carve_greedy(ar, c, B, S, max_len);
+  g.enc.status = cst;
   // the decode reads the workspace's copy of src_mask and writes the workspace's ids
   // (the captured graphs then depend on the workspace only); ids go out at the end
   HIPCHK(hipMemcpyAsync(g.mask, src_mask, (size_t)B * S, hipMemcpyDeviceToDevice, st));
   RC(greedy_run(m, g, src, B, S, max_len, start, f, st));
   HIPCHK(hipMemcpyAsync(ids, g.ids, (size_t)B * max_len * sizeof(int64_t),
                         hipMemcpyDeviceToDevice, st));
-  return status_publish(m, st);
+  return QTX_OK;
 }
 
 int32_t qtx_model_check(const qtx_model* m, void* stream) {
@@ -1445,10 +1439,13 @@ int32_t qtx_model_check(const qtx_model* m, void* stream) {
   DeviceGuard dg(m->device);
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   unsigned v = 0;
-  HIPCHK(hipMemcpy(&v, m->status_dev, sizeof v, hipMemcpyDeviceToHost));
-  v |= __atomic_exchange_n(m->status_host, 0u, __ATOMIC_ACQ_REL);
+  unsigned* word = nullptr;
+  for (const CallStatus& cs : t_calls)
+    if (cs.m == m && cs.serial == m->serial) word = cs.word;
+  if (!word) return QTX_OK;                 // no model-level call on this thread yet
+  HIPCHK(hipMemcpy(&v, word, sizeof v, hipMemcpyDeviceToHost));
   if (!v) return QTX_OK;
-  HIPCHK(hipMemset(m->status_dev, 0, sizeof(unsigned)));
+  HIPCHK(hipMemset(word, 0, sizeof(unsigned)));   // reported once
   return fail(QTX_E_DEVICE, "%s", status_text(v));
 }
 
@@ -1469,7 +1466,7 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
   const int D = c.d_model;
   const uint8_t* src_mask = g.mask;
   int64_t* ids = g.ids;
-  const bool fused = S <= 128 && max_len <= 128 && !env_flag("QTX_UNFUSED");
+  const bool fused = S <= 128 && max_len <= 128 && !knobs().unfused;
 
   // encoder: memory = encode(src_embed(src), src_mask); the cross K/V of every layer
   // (captured into a hipGraph with the steps' replay — QTX_PRE_GRAPH in round 3 — it
@@ -1513,7 +1510,7 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
       HIPCHK(hipStreamCreateWithFlags(&mm->gstream[i], hipStreamNonBlocking));
       HIPCHK(hipEventCreateWithFlags(&mm->ev_out[i], hipEventDisableTiming));
     }
-  if (env_flag("QTX_NO_GRAPH")) {     // eager launches (diagnostic); sub-batches on their streams
+  if (knobs().no_graph) {     // eager launches (QTX_NO_GRAPH); sub-batches on their streams
     const bool fk = gr.G > 1;
     if (fk) {
       HIPCHK(hipEventRecord(mm->ev_in, st));
@@ -1531,15 +1528,14 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
   // steps per graph: the whole decode in one graph by default (one graph launch); must
   // divide max_len-1 (the step position is read from device memory, so replays chain)
   int per_graph = max_len - 1;
-  if (const char* v = getenv("QTX_GRAPH_STEPS"))
-    if (*v && atoi(v) > 0 && (max_len - 1) % atoi(v) == 0) per_graph = atoi(v);
+  if (const int v = knobs().graph_steps; v > 0 && (max_len - 1) % v == 0) per_graph = v;
   if (max_len <= 1) return QTX_OK;
-  const bool joint = gr.G > 1 && env_flag("QTX_GROUP_GRAPH");
-  std::string variant;
-  for (const char* k : {"QTX_SPLIT_LN", "QTX_FFN_QKERNEL", "QTX_ABLATE", "QTX_ABLATE_NOP", "QTX_GROUP_GRAPH"}) {
-    const char* v = getenv(k);
-    variant += std::string(k) + "=" + (v ? v : "") + ";";
-  }
+  const bool joint = gr.G > 1 && knobs().group_graph;
+  // the switches a captured step depends on are part of its key (knobs can be reloaded)
+  const Knobs& kn = knobs();
+  const std::string variant = std::to_string(kn.split_ln) + std::to_string(kn.ffn_qkernel) + ":" +
+                              std::to_string(kn.ablate) + std::to_string(kn.ablate_nop) +
+                              std::to_string(kn.group_graph);
   const GraphKey key{B, S, max_len, gr.G * 1000 + per_graph, g.gsteps, variant};
   auto it = mm->graphs.find(key);
   if (it == mm->graphs.end()) {
@@ -1609,7 +1605,7 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
     for (int i = 0; i < gr.G; ++i) HIPCHK(hipStreamWaitEvent(ls[i], mm->ev_in, 0));
   }
   hipEvent_t tg0 = nullptr, tg1 = nullptr;   // QTX_TIME_GRAPH: diagnostic timing to stderr
-  const bool time_graph = env_flag("QTX_TIME_GRAPH");
+  const bool time_graph = knobs().time_graph;
   if (time_graph) {
     HIPCHK(hipEventCreate(&tg0));
     HIPCHK(hipEventCreate(&tg1));

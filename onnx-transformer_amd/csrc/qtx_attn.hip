@@ -27,6 +27,7 @@
 
 #include "qtx_common.h"
 #include "qtx_kernels.h"
+#include "qtx_knobs.h"
 
 QTX_STAMP_SETTER(attn)
 
@@ -566,10 +567,7 @@ hipError_t launch_attention_encq(const AttnArgs& a, int8_t* ctx8, float* sctx, h
   if (kp && a.c_ld != 512) return hipErrorInvalidValue;
   // all keys present and unmasked positions only differ through kadd/sks: the pipelined
   // head loop (QTX_ENCQ_NOPIPE=1: the sequential one, A/B)
-  static const bool nopipe = [] {
-    const char* v = getenv("QTX_ENCQ_NOPIPE");
-    return v && *v && *v != '0';
-  }();
+  const bool nopipe = knobs().encq_nopipe;    // QTX_DIAG build only
   if (a.Sk == AM_MAXK && !nopipe)
     k_attn_encq<true><<<dim3(a.B), dim3(512), 0, st>>>(a, ctx8, sctx, kp ? 1 : 0);
   else

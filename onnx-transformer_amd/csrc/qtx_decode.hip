@@ -17,6 +17,7 @@
 
 #include "qtx_common.h"
 #include "qtx_kernels.h"
+#include "qtx_knobs.h"
 
 QTX_STAMP_SETTER(decode)
 
@@ -492,10 +493,6 @@ hipError_t skinny_rb(const SkinnyArgs& g, int rb, hipStream_t st) {
     default: return hipErrorInvalidValue;
   }
 }
-int env_rb(const char* name, int def) {   // experiment overrides (QTX_RB_*)
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : def;
-}
 // Rows per workgroup (decode step, M = 32, measured in bench.py; tools/rb_sweep.sh: the
 // K = 512 int8 / F32Q row block 8 -> 4 took the step 234.8 -> 230.3 us): small row blocks spread
 // the A-panel and weight reads over more CUs — each CU sustains only a few KB in flight,
@@ -507,7 +504,8 @@ hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
   // 4.50 -> 3.67 and 5.26 -> 3.95 us per launch; at N = 512 the K-split one is faster
   // (64 workgroups of 32 KB each vs 256 of 8 KB: 3.09 vs 3.60 us).  QTX_SKINNY_WIDE=0: never,
   // =<rb>: every K = 512 launch (experiments).
-  static const int wide_env = env_rb("QTX_SKINNY_WIDE", -1);
+  const Knobs& kn = knobs();     // QTX_SKINNY_WIDE / QTX_RB_* / QTX_SKINNY8_MAXM: QTX_DIAG build
+  const int wide_env = kn.skinny_wide;
   const bool wide = wide_env < 0 ? (g.amode == A_LN && g.N >= 1024) : wide_env > 0;
   if (wide && g.K == 512 && g.N % 64 == 0) {
     const int rb = g.M <= 4 || wide_env <= 0 ? 4 : wide_env;
@@ -516,7 +514,7 @@ hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
     if (g.amode == A_F32Q) return skinny_wide_rb<WB, A_F32Q>(g, rb, st);
   }
   if (g.K == 512) {
-    static const int rb_i8 = env_rb("QTX_RB_I8_512", 4), rb_ln = env_rb("QTX_RB_LN", 4);
+    const int rb_i8 = kn.rb_i8_512, rb_ln = kn.rb_ln;
     if (g.amode == A_I8) return skinny_rb<512, WB, A_I8>(g, g.M <= 4 ? 4 : rb_i8, st);
     if (g.amode == A_LN) return skinny_rb<512, WB, A_LN>(g, rb_ln, st);
     if (g.amode == A_F32Q) return skinny_rb<512, WB, A_F32Q>(g, g.M <= 4 ? 4 : rb_i8, st);
@@ -524,12 +522,12 @@ hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
     // the decode FFN2 (fp32 hidden, residual, 8-bit weights) at M <= QTX_SKINNY8_MAXM
     // (default 32): 8 waves (measured: B = 32 decode 14.45 -> 14.40 ms; at B = 256 the
     // 4-wave kernel is faster, 35.1 vs 36.8 ms)
-    static const int sk8_maxm = env_rb("QTX_SKINNY8_MAXM", 32);
+    const int sk8_maxm = kn.skinny8_maxm;
     if (g.M <= sk8_maxm && WB == 8 && g.amode == A_F32Q && g.flags == EPI_RESIDUAL && g.pmax_n <= 128) {
       k_skinny8_ffn2<<<dim3(g.N / 16, (g.M + 3) / 4), 512, 0, st>>>(g);
       return hipGetLastError();
     }
-    static const int rb_i8 = env_rb("QTX_RB_I8_2048", 4), rb_f = env_rb("QTX_RB_F32Q", 4);
+    const int rb_i8 = kn.rb_i8_2048, rb_f = kn.rb_f32q;
     if (g.amode == A_I8) return skinny_rb<2048, WB, A_I8>(g, rb_i8, st);
     if (g.amode == A_F32Q) return skinny_rb<2048, WB, A_F32Q>(g, rb_f, st);
   }

@@ -308,11 +308,7 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
         const v4i afr = *reinterpret_cast<const v4i*>(As + r * KB + 16 * g_slot(r, fg));
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-#ifdef QTX_DIAG_NOMFMA
-          asm volatile("" ::"v"(afr), "v"(bfr[j]));
-#else
           acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, bfr[j], acc[i][j], 0, 0, 0);
-#endif
       }
     };
     uint8_t* s0 = lds;
@@ -321,36 +317,6 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
     uint8_t* s3 = lds + 3 * KSTG;
     // top of step kt: this wave's DMAs for kt retired (kt+1, kt+2 may still fly: 5 each),
     // the barrier makes every wave's part visible and frees stage (kt+3) % 4
-#ifdef QTX_KP_INTERLEAVE
-    // the 5 DMA pieces of step kt+3 spread between the MFMA groups of step kt
-    auto step = [&](uint8_t* cur, uint8_t* nxt3, int kt) {
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      int kk = min(kt + 3, nk - 1) + krot;
-      if (kk >= nk) kk -= nk;
-      const long k0 = (long)(kk + kb0) << 7;
-      const uint8_t* Bs = cur + KA;
-      v4i bfr[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int r = wn * 128 + j * 16 + fr;
-        bfr[j] = *reinterpret_cast<const v4i*>(Bs + r * KB + 16 * g_slot(r, fg));
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = wm * 64 + i * 16 + fr;
-        const v4i afr = *reinterpret_cast<const v4i*>(cur + r * KB + 16 * g_slot(r, fg));
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, bfr[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (i == 0) dma16(g.A + aoff + k0, nxt3 + wave * 16 * KB);
-        dma16(g.W + woff[i] + k0, nxt3 + KA + (wave * 64 + 16 * i) * KB);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-#else
     auto step = [&](uint8_t* cur, uint8_t* nxt3, int kt) {
       asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -358,7 +324,6 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
       issue(nxt3, kt + 3);
       compute(cur);
     };
-#endif
     issue(s0, 0);
     issue(s1, 1);
     issue(s2, 2);

@@ -154,6 +154,7 @@ struct RowGemmArgs {
   // per wait before giving up (0: the launcher's default).
   unsigned* status;
   int spin_limit;
+  int drop_slice;           // test hook (QTX_WSX_DROP_SLICE): this slice never publishes; -1
   // RE_RES_LN with kp at small M (at most 64 row tiles): split K over ksplit workgroups per
   // tile (int32 partials into part [ksplit][M][512], >= ksplit * M * 2 KB), then one wave per
   // row sums them and runs the residual + LayerNorm + quant epilogue.  0 / 1: no split.

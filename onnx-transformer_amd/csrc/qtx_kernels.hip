@@ -14,6 +14,7 @@
 
 #include "qtx_common.h"
 #include "qtx_kernels.h"
+#include "qtx_knobs.h"
 
 namespace qtx {
 
@@ -264,7 +265,7 @@ hipError_t launch_gemm(const GemmArgs& g, int wbits, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   if (g.K % 64 != 0 || (wbits != 8 && wbits != 4)) return hipErrorInvalidValue;
   const dim3 block(256);
-  if (wbits == 8 && !getenv("QTX_GEMM128")) {       // QTX_GEMM128: timing experiments only
+  if (wbits == 8 && !knobs().gemm128) {       // QTX_GEMM128 (QTX_DIAG build): timing experiments
     const hipError_t e = launch_gemm256(g, st);
     if (e != hipErrorNotSupported) return e;
   }
@@ -356,7 +357,7 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
   if (a.B <= 0 || a.Sq <= 0) return hipSuccess;
   if (!a.sk_dev && (a.Sk <= 0 || a.Sk > ATT_MAXK)) return hipErrorInvalidValue;
-  if (!getenv("QTX_ATTN_VALU")) {              // QTX_ATTN_VALU: timing experiments only
+  if (!knobs().attn_valu) {              // QTX_ATTN_VALU (QTX_DIAG build): timing experiments
     const hipError_t e = launch_attention_mfma(a, st);
     if (e != hipErrorNotSupported) return e;
   }

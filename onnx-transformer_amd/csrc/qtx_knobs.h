@@ -1,0 +1,64 @@
+// qtx_knobs.h — the library's environment switches, read ONCE (at the first launch that
+// consults them), never per launch.  Two kinds:
+//   * path switches of the product: alternative code paths the library carries for other
+//     shapes (two-pass FFN1, eager decode, unfused decoder, split K, ...) that the test suite
+//     forces at the shapes it tests, plus the hooks that make the FFN1 exchange's error path
+//     fire deterministically;
+//   * diagnostic switches (ablations, measured-negative kernels, timing aids): read only in the
+//     QTX_DIAG build (libqtx_diag.so, qtx/_build.py build(extra=...)); in the product build
+//     they are compile-time defaults and the variants they select are not compiled in.
+// qtx_debug_reload_knobs() (include/qtx.h) re-reads the environment: the tests that switch
+// paths within one process call it after changing a variable.
+#pragma once
+
+namespace qtx {
+
+struct Knobs {
+  // ---- product path switches
+  bool no_rowgemm = false;   // QTX_NO_ROWGEMM: the generic GEMM instead of the row GEMMs
+  bool no_splitk = false;    // QTX_NO_SPLITK: FFN2 at small M without the K split
+  bool no_wsx = false;       // QTX_NO_WSX: FFN1 in two passes instead of the in-launch exchange
+  bool no_kp = false;        // QTX_NO_KP: row GEMMs on the plain (non-KP) layout
+  bool no_attn_encq = false; // QTX_NO_ATTN_ENCQ: encoder attention without k_attn_encq
+  bool enc_nosplit = false;  // QTX_ENC_NOSPLIT: no two-stream encoder (two-pass FFN1 only)
+  bool unfused = false;      // QTX_UNFUSED: the unfused decoder step
+  bool no_graph = false;     // QTX_NO_GRAPH: eager decode launches
+  bool group_graph = false;  // QTX_GROUP_GRAPH: sub-batches as branches of one graph
+  bool split_ln = false;     // QTX_SPLIT_LN: separate LayerNorm kernels in the decode step
+  bool ffn_qkernel = false;  // QTX_FFN_QKERNEL: the FFN hidden quantized by its own kernel
+  bool ws_nopipe = false;    // QTX_WS_NOPIPE: the unpipelined weight-stationary kernel
+  bool wsr_off = false;      // QTX_WSR=0: the O-projection's WS epilogue on k_gemm_ws
+  int decode_groups = 0;     // QTX_DECODE_GROUPS: sub-batch graphs (0: by batch size)
+  int graph_steps = 0;       // QTX_GRAPH_STEPS: decode steps per graph (0: all)
+  long ws_min_m = 2048;      // QTX_WS_MIN_M: weight-stationary from this many rows
+  long ws_res_min_m = 2048;  // QTX_WS_RES_MIN_M / _MAX_M: the O-projection's WS range
+  long ws_res_max_m = 8192;
+  // ---- hooks of the FFN1 exchange's error path (tests/test_gpu_status.py)
+  int wsx_spin_limit = -1;   // QTX_WSX_SPIN_LIMIT: polls per wait (-1: the launcher's bound)
+  int wsx_drop_slice = -1;   // QTX_WSX_DROP_SLICE: this column slice never publishes its
+                             // row maxima, so its partners' waits time out (-1: none)
+  // ---- diagnostic switches (QTX_DIAG build only)
+  int ablate = 0;            // QTX_ABLATE: kernel classes dropped from the decode step
+  bool ablate_nop = false;   // QTX_ABLATE_NOP
+  bool dbg_tail = false;     // QTX_DBG_TAIL
+  bool time_graph = false;   // QTX_TIME_GRAPH
+  bool gemm128 = false;      // QTX_GEMM128
+  bool attn_valu = false;    // QTX_ATTN_VALU
+  bool encq_nopipe = false;  // QTX_ENCQ_NOPIPE
+  int wsq = 1;               // QTX_WSQ: 0 wsp, 1 wsq (product), 2 wss, 3 wsz, 4 wsa
+  int wsy = 1;               // QTX_WSY: 0 wsx, 1 wsy (product)
+  bool ws_prio = false;      // QTX_WS_PRIO
+  bool ws_xg = true;         // QTX_WS_XG
+  bool wsp_pmax_sr5 = false; // QTX_WSP_PMAX_SR5
+  bool wsa2 = false;         // QTX_WSA2
+  int skinny_wide = -1;      // QTX_SKINNY_WIDE
+  int rb_i8_512 = 4, rb_ln = 4, rb_i8_2048 = 4, rb_f32q = 4;   // QTX_RB_*
+  int skinny8_maxm = 32;     // QTX_SKINNY8_MAXM
+};
+
+// the switches, read from the environment on first use
+const Knobs& knobs();
+// re-read them (tests; not thread-safe against concurrent launches)
+void knobs_reload();
+
+}  // namespace qtx

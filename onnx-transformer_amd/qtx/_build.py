@@ -13,8 +13,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 REPO = os.path.dirname(os.path.dirname(HERE))
 LIB = os.path.join(HERE, "libqtx.so")
-SOURCES = ["qtx_kernels.hip", "qtx_decode.hip", "qtx_gemm.hip", "qtx_wsgemm.hip", "qtx_attn.hip", "qtx_api.hip"]
-HEADERS = ["qtx_common.h", "qtx_kernels.h"]
+SOURCES = ["qtx_kernels.hip", "qtx_decode.hip", "qtx_gemm.hip", "qtx_wsgemm.hip", "qtx_attn.hip",
+           "qtx_api.hip", "qtx_knobs.hip"]
+# measured-negative kernel variants and their switches: compiled only into the diagnostic
+# library (build(extra=...) -> libqtx_diag.so, with -DQTX_DIAG), never into libqtx.so
+DIAG_SOURCES = ["qtx_wsgemm_diag.hip"]
+HEADERS = ["qtx_common.h", "qtx_kernels.h", "qtx_ws.h", "qtx_knobs.h"]
 
 # -ffp-contract=off: every float op is a separate IEEE op (the numerics contract,
 # DESIGN.md §3); HIP keeps correctly rounded fp32 '/' and sqrtf by default.
@@ -49,6 +53,7 @@ def build(force: bool = False, verbose: bool = False, extra=()) -> str:
     cross-file device symbols), then linked into one shared library."""
     from concurrent.futures import ThreadPoolExecutor
     out = LIB if not extra else LIB.replace(".so", "_diag.so")
+    extra = list(extra) + (["-DQTX_DIAG"] if extra and "-DQTX_DIAG" not in extra else [])
     if not force and not extra and up_to_date():
         return LIB
     objdir = os.path.join(HERE, "build_obj")
@@ -65,8 +70,9 @@ def build(force: bool = False, verbose: bool = False, extra=()) -> str:
             raise RuntimeError(f"hipcc failed on {src} ({r.returncode}):\n{r.stderr[-4000:]}")
         return obj
 
-    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
-        objs = list(ex.map(compile_one, SOURCES))
+    srcs = SOURCES + (DIAG_SOURCES if extra else [])
+    with ThreadPoolExecutor(max_workers=min(len(srcs), os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, srcs))
     tmp = out + ".tmp"
     cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)

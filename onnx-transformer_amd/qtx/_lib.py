@@ -88,6 +88,7 @@ SIGNATURES = {
     "qtx_decode_attention": (I32, [I32, P, I64, P, P, P, P, I32, P, I32, P, I32, P, P, P]),
     "qtx_decode_argmax_embed": (I32, [P, P, I32, P, I64, P, P, P]),
     "qtx_debug_nop": (I32, [P]),
+    "qtx_debug_reload_knobs": (I32, []),
     "qtx_model_check": (I32, [P, P]),
 }
 
@@ -124,3 +125,9 @@ def call(name, *args):
     if rc != 0:
         raise QtxError(name, rc, L.qtx_last_error().decode(errors="replace"))
     return rc
+
+
+def reload_knobs():
+    """Re-read the library's environment switches (qtx_debug_reload_knobs): they are read
+    once per process otherwise (csrc/qtx_knobs.h)."""
+    lib().qtx_debug_reload_knobs()

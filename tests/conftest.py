@@ -46,3 +46,17 @@ def gpu_model(state_dict):
         pytest.skip("no GPU")
     from qtx.model import QtxModel
     return QtxModel(state_dict)
+
+
+@pytest.fixture
+def knob_env(monkeypatch):
+    """Set library switches (csrc/qtx_knobs.h, read once per process) for one test: sets the
+    variable and re-reads the switches; restores both at teardown."""
+    from qtx import _lib
+
+    def set_(name, value):
+        monkeypatch.setenv(name, str(value))
+        _lib.reload_knobs()
+    yield set_
+    monkeypatch.undo()
+    _lib.reload_knobs()

@@ -66,10 +66,13 @@ def cfg3_split(torch, gpu_model, cfg3_inputs):
     return _encode(torch, gpu_model, x, m)
 
 
-def test_cfg3_encoder_split_equals_single_stream(torch, gpu_model, cfg3_inputs, cfg3_split,
-                                                monkeypatch):
+def test_cfg3_encoder_two_pass_ffn1_equals_one_pass(torch, gpu_model, cfg3_inputs, cfg3_split,
+                                                   knob_env):
+    """The default encoder (one-pass FFN1 with the in-launch exchange, one stream) against
+    the two-pass FFN1 (QTX_NO_WSX), which also runs the batch as two half-batch streams: the
+    same bits."""
     x, m = cfg3_inputs
-    monkeypatch.setenv("QTX_ENC_NOSPLIT", "1")
+    knob_env("QTX_NO_WSX", 1)
     np.testing.assert_array_equal(_encode(torch, gpu_model, x, m), cfg3_split)
 
 

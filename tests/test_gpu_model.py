@@ -69,25 +69,25 @@ def test_greedy_decode_matches_oracle(torch, gpu_model, oracle_model, golden_mod
                                  {"QTX_DECODE_GROUPS": "2", "QTX_NO_GRAPH": "1"},
                                  {"QTX_DECODE_GROUPS": "2", "QTX_GROUP_GRAPH": "1"},
                                  {"QTX_SPLIT_LN": "1"}, {"QTX_FFN_QKERNEL": "1"}])
-def test_greedy_paths_agree(torch, gpu_model, monkeypatch, env):
+def test_greedy_paths_agree(torch, gpu_model, knob_env, env):
     """The fused+graph decode step, the fused eager step, the unfused kernels, graphs of
     several steps and sub-batches on several streams agree."""
     from qtx.decode import greedy_decode
     src, m = make_batch(np.random.default_rng(5), 5, 24, lens=[24, 20, 9, 17, 3])
     ref = greedy_decode(gpu_model, src, m, 40, 0)
     for k, v in env.items():
-        monkeypatch.setenv(k, v)
+        knob_env(k, v)
     np.testing.assert_array_equal(greedy_decode(gpu_model, src, m, 40, 0), ref)
 
 
-def test_greedy_default_groups_at_512(torch, gpu_model, monkeypatch):
+def test_greedy_default_groups_at_512(torch, gpu_model, knob_env):
     """From B = 512 the decode runs as two sub-batch graphs on two streams by default
     (qtx_api.hip decode_groups); its ids equal the one-graph decode's."""
     from qtx.decode import greedy_decode
     rng = np.random.default_rng(12)
     src, m = make_batch(rng, 512, 24, lens=list(rng.integers(3, 25, 512)))
     two = greedy_decode(gpu_model, src, m, 24, 0)
-    monkeypatch.setenv("QTX_DECODE_GROUPS", "1")
+    knob_env("QTX_DECODE_GROUPS", 1)
     np.testing.assert_array_equal(greedy_decode(gpu_model, src, m, 24, 0), two)
 
 

@@ -96,46 +96,81 @@ def test_concurrent_launches_bit_exact(torch, ffn1):
         assert scratch_flag(gx) == 0
 
 
-def test_timeout_flag_surfaces(torch, ffn1, monkeypatch):
-    """With the spin bound forced to one poll (QTX_WSX_SPIN_LIMIT=0) some wait finds a
-    partner's granule not yet published: the launch sets the status word instead of
-    passing a partial maximum off silently.  With the default bound it stays clear."""
+def test_timeout_flag_surfaces(torch, ffn1, knob_env):
+    """A wait that finds a partner's maxima missing must not pass a partial maximum off
+    silently: with the test hook that withholds slice 2's maxima (QTX_WSX_DROP_SLICE) and a
+    64-poll bound, every partner wait times out and the launch sets the status word — in one
+    run, deterministically.  With the default bound and no hook it stays clear."""
     base, h_ref, _ = ffn1
     st = torch.zeros(4, dtype=torch.int32, device="cuda")
     h8, _, _ = one_pass(torch, base, status=st)
     torch.cuda.synchronize()
     assert int(st[0].item()) == 0
     np.testing.assert_array_equal(h8.cpu().numpy(), h_ref)
-    monkeypatch.setenv("QTX_WSX_SPIN_LIMIT", "0")
-    flagged = 0
-    for _ in range(4):
-        st.zero_()
-        one_pass(torch, base, status=st)
-        torch.cuda.synchronize()
-        flagged += int(st[0].item()) & 1
-    assert flagged > 0, "no exchange wait timed out at a one-poll bound"
+    knob_env("QTX_WSX_SPIN_LIMIT", 64)
+    knob_env("QTX_WSX_DROP_SLICE", 2)
+    st.zero_()
+    one_pass(torch, base, status=st)
+    torch.cuda.synchronize()
+    assert int(st[0].item()) & 1, "the withheld partner maxima did not time out"
 
 
-def test_model_reports_device_error(torch, gpu_model, monkeypatch):
+def _cfg3(torch):
+    return (torch.randn((256, 128, 512), device="cuda"),
+            torch.ones((256, 128), dtype=torch.uint8, device="cuda"))
+
+
+def test_model_reports_device_error(torch, gpu_model, knob_env):
     """Through the model: an encoder run whose FFN1 exchange timed out makes
-    qtx_model_check (QtxModel.check) raise QTX_E_DEVICE = 5 once; the word is then clear."""
+    qtx_model_check (QtxModel.check) raise QTX_E_DEVICE = 5 once; the word is then clear,
+    and a clean run stays clean."""
     from qtx._lib import QtxError
-    x = torch.randn((256, 128, 512), device="cuda")
-    mk = torch.ones((256, 128), dtype=torch.uint8, device="cuda")
+    x, mk = _cfg3(torch)
     gpu_model.encode(x, mk)
     gpu_model.check()                                  # default bound: clean
-    monkeypatch.setenv("QTX_WSX_SPIN_LIMIT", "0")
-    raised = False
-    for _ in range(4):
-        gpu_model.encode(x, mk)
-        try:
-            gpu_model.check()
-        except QtxError as e:
-            assert e.code == 5 and "timed out" in str(e)
-            raised = True
-            break
-    assert raised
-    monkeypatch.delenv("QTX_WSX_SPIN_LIMIT")
+    knob_env("QTX_WSX_SPIN_LIMIT", 64)
+    knob_env("QTX_WSX_DROP_SLICE", 1)
+    gpu_model.encode(x, mk)
+    with pytest.raises(QtxError) as e:
+        gpu_model.check()
+    assert e.value.code == 5 and "timed out" in str(e.value)
     gpu_model.check()                                  # reported once, then cleared
+    knob_env("QTX_WSX_DROP_SLICE", -1)
     gpu_model.encode(x, mk)
     gpu_model.check()
+
+
+def test_status_word_is_per_call(torch, gpu_model, knob_env):
+    """the status word belongs to the call (its workspace), not to the model.
+    Thread A's cfg3 encode times out in its FFN1 exchange (hook on) while thread B encodes a
+    small batch concurrently (M = 288: the two-pass FFN1, no exchange) and checks on its own
+    stream: B's check is clean and cannot clear A's error; A's check raises."""
+    import threading
+    from qtx._lib import QtxError
+    knob_env("QTX_WSX_SPIN_LIMIT", 64)
+    knob_env("QTX_WSX_DROP_SLICE", 3)
+    xa, ma = _cfg3(torch)
+    xb = torch.randn((4, 72, 512), device="cuda")
+    mb = torch.ones((4, 72), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    res = {}
+    go = threading.Barrier(2)
+
+    def run(name, x, m):
+        try:
+            with torch.cuda.stream(torch.cuda.Stream()):
+                go.wait()
+                for _ in range(3 if name == "b" else 1):
+                    gpu_model.encode(x, m)
+                    gpu_model.check()
+            res[name] = "clean"
+        except QtxError as e:
+            res[name] = e.code
+        except Exception as e:             # noqa: BLE001 - reported below
+            res[name] = repr(e)
+    ts = [threading.Thread(target=run, args=("a", xa, ma)), threading.Thread(target=run, args=("b", xb, mb))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert res == {"a": 5, "b": "clean"}, res
