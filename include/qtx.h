@@ -118,9 +118,10 @@ int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t*
                           int32_t B, int32_t S, int32_t max_len, int64_t start, int64_t* ids,
                           void* ws, size_t ws_bytes, void* stream);
 
-/* Synchronise `stream`, then report (and clear) the model's device status word: QTX_OK, or
- * QTX_E_DEVICE if a kernel of an earlier call on this model flagged an error (the outputs
- * of that call are invalid).  The Python layer calls it wherever it synchronises anyway. */
+/* Synchronise `stream`, then report (and clear) the calling thread's device status word on
+ * this model: QTX_OK, or QTX_E_DEVICE if a kernel of the thread's last model-level call on it
+ * flagged an error (the outputs of that call are invalid; every model-level call zeroes the
+ * word first).  The Python layer calls it wherever it synchronises anyway. */
 int32_t qtx_model_check(const qtx_model* m, void* stream);
 
 /* ---- fault injection (the reference's campaigns: inject_utils/layers.py:48-84,

@@ -123,6 +123,8 @@ struct qtx_model {
   hipEvent_t ev_fork = nullptr, ev_lag = nullptr, ev_join = nullptr;
   int device = 0;            // the device the model's memory lives on
   unsigned long long serial = 0;   // unique per created model (call status records)
+  unsigned* status = nullptr;      // kStatusSlots 16-byte status words (model memory)
+  std::atomic<int> next_status{0};
   // an exec may still be running on a caller's stream: wait for its last replay first
   void clear_graphs() {
     for (auto& kv : graphs) {
@@ -160,13 +162,15 @@ const char* status_text(unsigned v) {
                "FFN hidden was quantized from a partial row maximum): outputs invalid"
              : "device status word set";
 }
-// Every model-level call has its OWN status word: the first 256 bytes of its workspace
-// (the caller's memory: one workspace per calling thread, include/qtx.h).  The call zeroes
-// it on its stream before its kernels run; a kernel that detects an error it cannot repair
-// (k_gemm_wsy's exchange timeout) ORs a DEV_E_* bit into it.  qtx_model_check(m, stream)
-// synchronises the stream and reads the word of the calling thread's last call on m, so an
-// error is reported to the thread whose call raised it and no other thread's call can clear
-// it (one word per model let another thread's check wipe it).
+// Status words live in the model's own memory: kStatusSlots 16-byte words, one per calling
+// thread (a thread's first model-level call on a model claims the next slot; past
+// kStatusSlots threads, slots are shared round robin).  Every model-level call zeroes its
+// thread's word on its stream before its kernels run; a kernel that detects an error it
+// cannot repair (k_gemm_wsy's exchange timeout) ORs a DEV_E_* bit into it.
+// qtx_model_check(m, stream) synchronises the stream and reads the calling thread's word,
+// so an error is reported to the thread whose call raised it and no other thread's call can
+// clear it, and no later use of a caller's workspace can overwrite it.
+constexpr int kStatusSlots = 64;
 struct CallStatus {
   const qtx_model* m = nullptr;
   unsigned long long serial = 0;    // the model's creation serial (a new model at a freed
@@ -176,17 +180,20 @@ constexpr int kCallSlots = 8;
 thread_local CallStatus t_calls[kCallSlots];
 thread_local int t_next = 0;
 
-unsigned* take_call_status(Arena& ar) { return ar.take<unsigned>(64); }
-
-int call_status_begin(const qtx_model* m, unsigned* word, hipStream_t st) {
-  HIPCHK(launch_zero(word, sizeof(unsigned), st));     // a kernel: graph-capturable, ordered
+unsigned* thread_status_word(qtx_model* m) {
   for (CallStatus& c : t_calls)
-    if (c.m == m && c.serial == m->serial) {
-      c.word = word;
-      return QTX_OK;
-    }
-  t_calls[t_next] = CallStatus{m, m->serial, word};
+    if (c.m == m && c.serial == m->serial) return c.word;
+  unsigned* w = m->status + 4 * (m->next_status.fetch_add(1) % kStatusSlots);
+  t_calls[t_next] = CallStatus{m, m->serial, w};
   t_next = (t_next + 1) % kCallSlots;
+  return w;
+}
+
+// the calling thread's word, zeroed on st (a kernel: graph-capturable, stream-ordered)
+int call_status_begin(const qtx_model* mc, unsigned** word, hipStream_t st) {
+  qtx_model* m = const_cast<qtx_model*>(mc);
+  *word = thread_status_word(m);
+  HIPCHK(launch_zero(*word, 16, st));
   return QTX_OK;
 }
 
@@ -293,6 +300,7 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     float* gb = ar.take<float>(c.tgt_vocab);
     int8_t* tmp = ar.take<int8_t>((size_t)F * D);
     m->gen_wt = ar.take<float>((size_t)((c.tgt_vocab + 15) / 16) * 16 * D);
+    m->status = ar.take<unsigned>(4 * kStatusSlots);
     return std::make_tuple(norms, src_lut, tgt_lut, pe_d, gw, gb, tmp);
   };
   qtx_model* m = new qtx_model();
@@ -317,6 +325,10 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
   float *norms, *src_lut, *tgt_lut, *pe_d, *gw, *gb;
   int8_t* tmp;
   std::tie(norms, src_lut, tgt_lut, pe_d, gw, gb, tmp) = carve(m, ar);
+  if (hipMemset(m->status, 0, 16 * kStatusSlots) != hipSuccess) {
+    qtx_model_destroy(m);
+    return fail(QTX_E_HIP, "hipMemset(status words)");
+  }
 
   int rc = QTX_OK;
   auto Q = [&](QLin& L, int row0, int ti, int N, int K) {
@@ -903,11 +915,9 @@ bool enc_split(int B) { return B >= 256 && !knobs().enc_nosplit && !wsx_on(); }
 
 size_t enc_ws(const qtx_config& c, int B, int S) {
   Arena ar;
-  take_call_status(ar);
   carve_scratch(ar, c, (long)B * S);
   if (enc_split(B)) {
     Arena a2;
-    take_call_status(a2);
     carve_scratch(a2, c, (long)(B / 2) * S);
     carve_scratch(a2, c, (long)(B - B / 2) * S);
     ar.used = std::max(ar.used, a2.used);
@@ -1237,7 +1247,6 @@ size_t qtx_decoder_workspace_size(const qtx_model* m, int32_t B, int32_t T, int3
 size_t qtx_greedy_workspace_size(const qtx_model* m, int32_t B, int32_t S, int32_t max_len) {
   if (!m) return 0;
   Arena ar;
-  take_call_status(ar);
   carve_greedy(ar, m->cfg, B, S, max_len);
   return align_up(ar.used);
 }
@@ -1252,8 +1261,8 @@ int32_t qtx_encoder_forward_fault(const qtx_model* m, const float* x, const uint
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
   hipStream_t st = (hipStream_t)stream;
-  unsigned* cst = take_call_status(ar);
-  RC(call_status_begin(m, cst, st));
+  unsigned* cst = nullptr;
+  RC(call_status_begin(m, &cst, st));
   if (!enc_split(B) || (f && f->kind != QTX_FAULT_NONE)) {
     Scratch s = carve_scratch(ar, m->cfg, (long)B * S);
     s.status = cst;
@@ -1308,9 +1317,12 @@ int32_t qtx_decoder_forward_fault(const qtx_model* m, const float* y, const floa
   hipStream_t st = (hipStream_t)stream;
   const qtx_config& c = m->cfg;
   const int D = c.d_model, M = B * T;
+  unsigned* cst = nullptr;
+  RC(call_status_begin(m, &cst, st));
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
   Scratch s = carve_scratch(ar, c, M);
+  s.status = cst;
   CrossKV x = carve_cross(ar, c, (long)B * S);
   RC(cross_kv(m, memory, B * S, x, st, f));
   HIPCHK(hipMemcpyAsync(s.x, y, (size_t)M * D * 4, hipMemcpyDeviceToDevice, st));
@@ -1421,8 +1433,8 @@ int32_t qtx_greedy_decode_fault(const qtx_model* m, const int64_t* src,
   hipStream_t st = (hipStream_t)stream;
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
-  unsigned* cst = take_call_status(ar);
-  RC(call_status_begin(m, cst, st));
+  unsigned* cst = nullptr;
+  RC(call_status_begin(m, &cst, st));
   GreedyWS g = carve_greedy(ar, c, B, S, max_len);
   g.enc.status = cst;
   // the decode reads the workspace's copy of src_mask and writes the workspace's ids
@@ -1445,7 +1457,7 @@ int32_t qtx_model_check(const qtx_model* m, void* stream) {
   if (!word) return QTX_OK;                 // no model-level call on this thread yet
   HIPCHK(hipMemcpy(&v, word, sizeof v, hipMemcpyDeviceToHost));
   if (!v) return QTX_OK;
-  HIPCHK(hipMemset(word, 0, sizeof(unsigned)));   // reported once
+  HIPCHK(hipMemset(word, 0, sizeof(unsigned)));   // reported once (the thread's own word)
   return fail(QTX_E_DEVICE, "%s", status_text(v));
 }
 

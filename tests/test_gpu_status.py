@@ -141,7 +141,7 @@ def test_model_reports_device_error(torch, gpu_model, knob_env):
 
 
 def test_status_word_is_per_call(torch, gpu_model, knob_env):
-    """the status word belongs to the call (its workspace), not to the model.
+    """the status word belongs to the calling thread, not to the model as a whole.
     Thread A's cfg3 encode times out in its FFN1 exchange (hook on) while thread B encodes a
     small batch concurrently (M = 288: the two-pass FFN1, no exchange) and checks on its own
     stream: B's check is clean and cannot clear A's error; A's check raises."""
