@@ -489,12 +489,38 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (h < 8) convert_v(std::integral_constant<int, (h < 8 ? h : 0)>{});
       float xn[8][4];
-      if constexpr (h < 8) {
-        const v4i qcur = qf;
-        if (h < 7) qf = *reinterpret_cast<const v4i*>(qbase + 64 * (h + 1));   // next head
-        scores_softmax(std::integral_constant<int, (h < 8 ? h : 0)>{}, qcur, xn, full_t{});
+      auto sm = [&]() {
+        if constexpr (h < 8) {
+          const v4i qcur = qf;
+          if (h < 7) qf = *reinterpret_cast<const v4i*>(qbase + 64 * (h + 1));   // next head
+          scores_softmax(std::integral_constant<int, (h < 8 ? h : 0)>{}, qcur, xn, full_t{});
+        }
+      };
+      auto pvp = [&]() {
+        if constexpr (h >= 1) pv_f(std::integral_constant<int, (h >= 1 ? h - 1 : 0)>{}, xp);
+      };
+#if defined(QTX_EXP_ATTN_DESYNC) && QTX_EXP_ATTN_DESYNC == 2
+      // separated phases, the same order on every wave: the PV of head h-1 (its P then
+      // dies), then the scores and softmax of head h
+      pvp();
+      __builtin_amdgcn_sched_barrier(0);
+      sm();
+#elif defined(QTX_EXP_ATTN_DESYNC)
+      // the two waves of a SIMD in opposite phases: waves 0-3 softmax then PV, waves 4-7 PV
+      // then softmax, so one wave's f32 MFMAs run beside the other's VALU
+      if (wave < 4) {
+        sm();
+        __builtin_amdgcn_sched_barrier(0);
+        pvp();
+      } else {
+        pvp();
+        __builtin_amdgcn_sched_barrier(0);
+        sm();
       }
-      if constexpr (h >= 1) pv_f(std::integral_constant<int, (h >= 1 ? h - 1 : 0)>{}, xp);
+#else
+      sm();
+      pvp();
+#endif
       if constexpr (h < 8) {
 #pragma unroll
         for (int kt = 0; kt < 8; ++kt)
