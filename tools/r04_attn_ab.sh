@@ -17,3 +17,4 @@ cat $O/ab.log
 for L in $P $D; do
   QTX_LIB_PATH=$L timeout -k 10 200 python tools/enc_bench.py 2>&1 | grep -i encoder | sed "s|^|$(basename $L) |" || exit 1
 done
+timeout -k 10 120 python tools/mall_probe.py 2>&1 | grep -v amdgpu.ids | tee $O/mall_probe.log || exit 1
