@@ -472,9 +472,8 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
       pv(hc, x, part_t{});
     });
   } else {
-    // all 128 keys present: software pipelined — iteration h runs the scores and softmax
-    // of head h (VALU-bound) and the PV of head h-1 (f32 MFMA-bound) in one basic block,
-    // so the compiler interleaves the two (measured unpipelined: no overlap)
+    // all 128 keys present: pipelined over heads — iteration h runs the PV of head h-1
+    // (f32 MFMA) and then the scores and softmax of head h (VALU)
     // V of head h is converted in iteration h (into buffer h & 1, last read by the PV of
     // head h - 2 in iteration h - 1) and read by the PV of head h in iteration h + 1: one
     // barrier at the top of each iteration orders both
@@ -499,28 +498,14 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
       auto pvp = [&]() {
         if constexpr (h >= 1) pv_f(std::integral_constant<int, (h >= 1 ? h - 1 : 0)>{}, xp);
       };
-#if defined(QTX_EXP_ATTN_DESYNC) && QTX_EXP_ATTN_DESYNC == 2
-      // separated phases, the same order on every wave: the PV of head h-1 (its P then
-      // dies), then the scores and softmax of head h
+      // the PV of head h-1 first (its P dies there), then the scores and softmax of head h,
+      // as two phases: the f32 MFMA and the VALU share the SIMD's vector datapath
+      // (profiles/r04_f32_split_probe.log), so interleaving them buys no overlap; in this
+      // order the previous and the next P are never live together (no spill; 82.9 -> 81.6 us
+      // at cfg3, A/B in gpurun_out/r04at2; waves of a SIMD in opposite phase orders: 86 us)
       pvp();
       __builtin_amdgcn_sched_barrier(0);
       sm();
-#elif defined(QTX_EXP_ATTN_DESYNC)
-      // the two waves of a SIMD in opposite phases: waves 0-3 softmax then PV, waves 4-7 PV
-      // then softmax, so one wave's f32 MFMAs run beside the other's VALU
-      if (wave < 4) {
-        sm();
-        __builtin_amdgcn_sched_barrier(0);
-        pvp();
-      } else {
-        pvp();
-        __builtin_amdgcn_sched_barrier(0);
-        sm();
-      }
-#else
-      sm();
-      pvp();
-#endif
       if constexpr (h < 8) {
 #pragma unroll
         for (int kt = 0; kt < 8; ++kt)
