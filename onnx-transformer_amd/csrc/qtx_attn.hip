@@ -478,7 +478,7 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
     // head h - 2 in iteration h - 1) and read by the PV of head h in iteration h + 1: one
     // barrier at the top of each iteration orders both
     float xp[8][4];
-    long long st_bar = 0;                          // QTX_STAMPS builds only: barrier wait
+    long long st_bar = 0, st_pv = 0, st_sm = 0, st_cv = 0;   // QTX_STAMPS builds only
     static_for<9>([&](auto hc) {
       constexpr int h = decltype(hc)::value;
       const long long tb0 = QTX_NOW();
@@ -486,7 +486,9 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
       st_bar += QTX_NOW() - tb0;
       QTX_STAMP(4 + h);
       __builtin_amdgcn_sched_barrier(0);
+      const long long tc0 = QTX_NOW();
       if constexpr (h < 8) convert_v(std::integral_constant<int, (h < 8 ? h : 0)>{});
+      st_cv += QTX_NOW() - tc0;
       float xn[8][4];
       auto sm = [&]() {
         if constexpr (h < 8) {
@@ -503,9 +505,16 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
       // (profiles/r04_f32_split_probe.log), so interleaving them buys no overlap; in this
       // order the previous and the next P are never live together (no spill; 82.9 -> 81.6 us
       // at cfg3, A/B in gpurun_out/r04at2; waves of a SIMD in opposite phase orders: 86 us)
-      pvp();
-      __builtin_amdgcn_sched_barrier(0);
-      sm();
+      {
+        const long long tp0 = QTX_NOW();
+        pvp();
+        __builtin_amdgcn_sched_barrier(0);
+        const long long tp1 = QTX_NOW();
+        sm();
+        __builtin_amdgcn_sched_barrier(0);
+        st_pv += tp1 - tp0;
+        st_sm += QTX_NOW() - tp1;
+      }
       if constexpr (h < 8) {
 #pragma unroll
         for (int kt = 0; kt < 8; ++kt)
@@ -514,8 +523,12 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
       }
     });
 #ifdef QTX_STAMPS
-    // per wave (lane 0): barrier wait over the head loop, at [4096 + 2 (8 block + wave)]
-    if (lane == 0 && qtx_stamp_buf) qtx_stamp_buf[4096 + 2 * (b * 8 + wave)] = st_bar;
+    // per wave (lane 0), summed over the head loop: barrier wait, PV, scores + softmax,
+    // V conversion, at [4096 + 4 (8 block + wave) + 0..3]
+    if (lane == 0 && qtx_stamp_buf) {
+      unsigned long long* pw = qtx_stamp_buf + 4096 + 4 * (b * 8 + wave);
+      pw[0] = st_bar; pw[1] = st_pv; pw[2] = st_sm; pw[3] = st_cv;
+    }
 #endif
   }
   QTX_STAMP(2);

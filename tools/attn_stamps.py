@@ -33,6 +33,7 @@ d = lambda a, b: np.median(st[:, b] - st[:, a])
 print("staging", d(0, 1), "heads", d(1, 2), "quant+store", d(2, 3))
 print("per head iteration (wave 0, after the barrier):", [round(d(4 + h, 5 + h)) for h in range(8)],
       "last PV", d(12, 2))
-bar = buf.view(-1)[4096:4096 + 2 * B * 8:2].cpu().numpy().reshape(B, 8).astype(np.float64)
-print("barrier wait over the head loop per wave (median over WGs):", np.median(bar, axis=0).round())
+pw = buf.view(-1)[4096:4096 + 4 * B * 8].cpu().numpy().reshape(B, 8, 4).astype(np.float64)
+for i, name in enumerate(["barrier wait", "PV", "scores+softmax", "V convert"]):
+    print(f"{name:15s} over the head loop per wave (median over WGs):", np.median(pw[:, :, i], axis=0).round())
 print("total span", (st[:, 3].max() - st[:, 0].min()), "cyc; median WG", d(0, 3))
