@@ -941,11 +941,15 @@ template <int PRIO = 0, int LAG = 1>   // as k_gemm_wsq
 __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
   constexpr int SR = WS_SR, WL = 8 * (8 - SR) * 4 * 1024;
   // LDS: 2 A stages (32 KB) | W K steps 5-7 (96 KB) | sw, bias (4 KB) | red [2][8][32] (2 KB)
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4 + 2 * 8 * 64 * 4];
+  // | row scales [2][8][64] (4 KB) | full row maxima [2][32]
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4 + 2 * 8 * 64 * 4 +
+                                                      2 * 2 * WP_R * 4];
   uint8_t* const wl = lds + 2 * WP_STAGE;
   float* const swl = reinterpret_cast<float*>(wl + WL);
   float* const red0 = swl + 1024;                            // [2][8][32]
   float* const sal = red0 + 2 * 8 * WP_R;                    // [2][8 waves][64]: row scales
+  float* const gsc = sal + 2 * 8 * 64;                       // [2][2][32]: rows' scale s and
+                                                             // RN(1/s) per block parity
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int f = lane & 15, gq = lane >> 4;
   const int nb = (g.M + WP_R - 1) / WP_R;
@@ -1086,23 +1090,23 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
   };
   // block k's scale from its full row maximum m (stored; lane: row lane & 31), broadcast per
   // row fragment: divisor bq, reciprocal iq
-  auto scales = [&](int k, float m, float (&bq)[2], float (&iq)[2]) {
-    const float sc = fmaxf(m, 1e-5f) / 127.0f;
-    const float inv = 1.0f / sc;
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc), srsrc, 4 * (rbk(k) * WP_R + (lane & 31)), 0, 0);
+  // block k's row scales (s and RN(1/s), written by wave 0 before this iteration's
+  // barrier, gather_scales below) for the lane's rows of each row fragment
+  auto scales = [&](int k, float (&bq)[2], float (&iq)[2]) {
+    const float* gs = gsc + (k & 1) * 2 * WP_R;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      bq[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(sc)));
-      iq[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (16 * i + f), __float_as_int(inv)));
+      bq[i] = gs[16 * i + f];
+      iq[i] = gs[WP_R + 16 * i + f];
     }
   };
   auto store_row = [&](int k, int i, const uint32_t (&d)[4]) {
     const long row = rbk(k) * WP_R + 16 * i + f;
     __builtin_amdgcn_raw_buffer_store_b128(v4u{d[0], d[1], d[2], d[3]}, orsrc, (int)kp_off(row, c0, g.ldo8), 0, 0);
   };
-  auto quant_all = [&](int k, const float (&y)[2][16], float m) {      // 3 stores
+  auto quant_all = [&](int k, const float (&y)[2][16]) {      // 2 stores (+ wave 0's scale)
     float bq[2], iq[2];
-    scales(k, m, bq, iq);
+    scales(k, bq, iq);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       uint32_t d[4];
@@ -1116,11 +1120,11 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
     }
   };
   // M(k) into acc; Q: block kq's quantization (y, full maximum m) pinned between the MFMAs
-  auto mfma_block = [&](v4i (&acc)[2][4], int k, auto q_c, int kq, float (&y)[2][16], float m) {
+  auto mfma_block = [&](v4i (&acc)[2][4], int k, auto q_c, int kq, float (&y)[2][16]) {
     constexpr bool Q = decltype(q_c)::value;
     const uint8_t* cur = lds + (k & 1) * WP_STAGE;
     float bq[2] = {0.0f, 0.0f}, iq[2] = {0.0f, 0.0f};
-    if constexpr (Q) scales(kq, m, bq, iq);
+    if constexpr (Q) scales(kq, bq, iq);
     float hist[3] = {0.0f, 0.0f, 0.0f}, tq[4];   // results of the last outputs, newest first
     uint32_t d[4];
 #pragma unroll
@@ -1178,17 +1182,17 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
       __builtin_amdgcn_s_barrier();
     }
     const long long t1 = QTX_NOW();
-    float m2 = 0.0f;
-    if (k >= 2) m2 = full_max(k - 2, mb);       // granule loads: before this iteration's DMA
+    // (block k-2's row scales: gathered by wave 0 at the end of iteration k-1 from the
+    // maxima its partners published an iteration before that; read after the barrier)
     const long long t2 = QTX_NOW();
-    if (k >= 1 && k <= nblk) {
+    if (wave == 0 && k >= 1 && k <= nblk) {     // only wave 0 publishes and gathers
       mo = slice_max(k - 1);
       publish(k - 1, mo);
     }
     if (k + 1 < nblk) issue(k + 1);
     if (k < nblk) {
-      if (k >= 2) mfma_block(acc, k, T_, k - 2, yb, m2);
-      else mfma_block(acc, k, F_, 0, yb, 0.0f);
+      if (k >= 2) mfma_block(acc, k, T_, k - 2, yb);
+      else mfma_block(acc, k, F_, 0, yb);
       const long long t3 = QTX_NOW();
       form_y(acc, yb, k);
       if (k >= 2) {
@@ -1198,9 +1202,27 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
         st_y += QTX_NOW() - t3;
       }
     } else if (k >= 2) {
-      quant_all(k - 2, yb, m2);
+      quant_all(k - 2, yb);
     } else {
       dummy_stores();
+    }
+    // wave 0 (a SIMD arbitration winner: it reaches the next barrier ~1,300 cycles before
+    // the losers) gathers block k-1's partner maxima now, so the load latency hides in its
+    // barrier slack instead of opening every wave's next iteration
+    // and turns them into the block's row scales (s = max(m, 1e-5) / 127, stored for the
+    // next GEMM; RN(1/s) for div_cr) once, for every wave
+    if (wave == 0 && k >= 1 && k <= nblk) {
+      const long long tf0 = QTX_NOW();
+      const float m = full_max(k - 1, mo);
+      const float sc = fmaxf(m, 1e-5f) / 127.0f;
+      const float inv = 1.0f / sc;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc), srsrc, 4 * (rbk(k - 1) * WP_R + (lane & 31)), 0, 0);
+      if (lane < WP_R) {
+        float* gs = gsc + ((k - 1) & 1) * 2 * WP_R;
+        gs[lane] = sc;
+        gs[WP_R + lane] = inv;
+      }
+      st_fm += QTX_NOW() - tf0;
     }
   };
   for (int k = 0; k <= nblk + 1; k += 2) {
