@@ -922,20 +922,23 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
 // =====================================================================================
 // k_gemm_wsy: the one-pass FFN1 of k_gemm_wsx with k_gemm_wsq's schedule — ONE barrier per
 // 32-row block and the quantization between the MFMAs (asm statements, pinned):
-//   iteration k:  top barrier (block k-1's partial row maxima complete in red[(k-1) & 1]);
-//                 the row maxima of block k-2 over all 4 slices (the partners published
-//                 them an iteration ago); block k-1's slice maxima published; block k+1's
-//                 A by LDS-DMA; the 64 MFMAs of block k with block k-2's quantized outputs
-//                 pinned between them; y = relu(((acc * sa) * sw) + b) of block k and its
-//                 partial row maxima -> red[k & 1] (VALU-only phase).
+//   iteration k:  top barrier (block k-1's partial row maxima complete in red[(k-1) & 1],
+//                 block k-2's row scales in LDS); wave 0 publishes block k-1's slice
+//                 maxima; block k+1's A by LDS-DMA; the 64 MFMAs of block k with block
+//                 k-2's quantized outputs pinned between them; y = relu(((acc * sa) * sw)
+//                 + b) of block k and its partial row maxima -> red[k & 1] (VALU-only
+//                 phase); then wave 0 alone gathers block k-1's maxima over all 4 slices
+//                 (its partners published them an iteration ago) and forms that block's
+//                 row scales for every wave — in the ~1,300 cycles by which wave 0, a SIMD
+//                 arbitration winner, reaches the next barrier before the losers.
 // y of blocks k-1 and k-2 are both held (one buffer per block parity): the quantization of
 // block k waits two iterations for its partners' maxima, so the hand-off latency hides under
 // a whole iteration as in k_gemm_wsx.  The exchange (tickets, granules, bounded waits that
 // report DEV_E_EXCHANGE_TIMEOUT) is k_gemm_wsx's.  Numerics as k_gemm_wsq: RN(y / s) by
 // div_cr with the row's reciprocal, s by true division.
-// Wait ordering: the granule loads (waited for at once) go before this iteration's DMA and
-// stores; the top of an iteration waits vmcnt(0) (VM_CNT_ORDER, qtx_common.h: a store may
-// retire before a DMA issued ahead of it, so counting the stores behind the DMA is unsafe).
+// Wait ordering: the top of an iteration waits vmcnt(0) (VM_CNT_ORDER, qtx_common.h: a store
+// may retire before a DMA issued ahead of it, so counting the stores behind the DMA is
+// unsafe); wave 0's granule loads are waited for where it gathers them.
 // =====================================================================================
 template <int PRIO = 0, int LAG = 1>   // as k_gemm_wsq
 __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
