@@ -174,3 +174,24 @@ def test_status_word_is_per_call(torch, gpu_model, knob_env):
     for t in ts:
         t.join(timeout=120)
     assert res == {"a": 5, "b": "clean"}, res
+
+
+def test_workspace_reuse_reports_no_false_error(torch, gpu_model):
+    """Round 4: the status word first lived in the call's workspace; the next call on the
+    same workspace (the decoder-fault greedy loop: an encode, then decoder calls) wrote its
+    scratch over it and a check read that as an error.  The word now lives in the model's
+    memory, per thread: an encode followed by a decoder call on the thread's one (reused)
+    workspace, filled with nonzero bytes first, checks clean after each call."""
+    x = torch.randn((2, 16, 512), device="cuda")
+    m = torch.ones((2, 16), dtype=torch.uint8, device="cuda")
+    nb = max(int(gpu_model.workspace(0).numel()), 1 << 20)
+    gpu_model.workspace(nb).fill_(0xFF)
+    mem = gpu_model.encode(x, m)
+    gpu_model.check()
+    y = torch.randn((2, 5, 512), device="cuda")
+    tm = torch.tril(torch.ones((5, 5), dtype=torch.uint8, device="cuda"))
+    gpu_model.workspace(nb).fill_(0xFF)
+    gpu_model.decode(y, mem, m, tm)
+    gpu_model.check()
+    gpu_model.encode(x, m)
+    gpu_model.check()
