@@ -47,10 +47,10 @@ typedef enum {
   QTX_E_HIP = 2,       /* a HIP runtime error, message in qtx_last_error() */
   QTX_E_WORKSPACE = 3, /* workspace too small: see qtx_*_workspace_size */
   QTX_E_UNSUPPORTED = 4,
-  QTX_E_DEVICE = 5     /* a kernel flagged an error it cannot repair in the model's device
-                        * status word (k_gemm_wsx: FFN1 row-max exchange timed out, outputs
-                        * invalid); reported by qtx_model_check, or by the next model-level
-                        * call on the model once the earlier call's work has finished */
+  QTX_E_DEVICE = 5     /* a kernel flagged an error it cannot repair in the calling
+                        * thread's device status word on the model (k_gemm_wsx: FFN1 row-max
+                        * exchange timed out, outputs invalid); reported by qtx_model_check
+                        * (the thread's next model-level call on the model zeroes the word) */
 } qtx_status;
 
 typedef struct qtx_model qtx_model;

@@ -89,8 +89,8 @@ class QtxModel:
     @_on_device
     def check(self):
         """Synchronise the current stream and raise QtxError (status QTX_E_DEVICE) if a
-        kernel of an earlier call flagged an error in the model's device status word
-        (qtx_model_check); called wherever the host synchronises anyway."""
+        kernel of this thread's last call on the model flagged an error in the thread's
+        device status word (qtx_model_check); called wherever the host synchronises anyway."""
         _lib.call("qtx_model_check", self.handle, _stream(self.device))
 
     @property
