@@ -595,6 +595,10 @@ def main():
             del m4
             t5 = time_decode(model, 256, S, L)
             out["cfg5_per_gpu_decode"] = {"B": 256, "ms": t5 * 1e3, "tokens_per_s": 256 * (L - 1) / t5}
+            # cfg1's shape (one sentence, the reference's own CPU-runnable case) on the GPU:
+            # the latency of one greedy decode, beside cpu_baseline's cfg1 leg
+            t1 = time_decode(model, 1, S, L)
+            out["cfg1_b1_decode"] = {"B": 1, "ms": t1 * 1e3, "tokens_per_s": (L - 1) / t1}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(sd)
         print(json.dumps(out))
