@@ -176,7 +176,8 @@ struct CallStatus {
   unsigned long long serial = 0;    // the model's creation serial (a new model at a freed
   unsigned* word = nullptr;         // address is a different model)
 };
-constexpr int kCallSlots = 8;
+constexpr int kCallSlots = 32;     // models a thread keeps its word for (round robin past it:
+                                   // the next call on an evicted model claims a new word)
 thread_local CallStatus t_calls[kCallSlots];
 thread_local int t_next = 0;
 
