@@ -2,7 +2,8 @@
 // v_mfma_i32_16x16x64_i8 at its full rate, and does it matter where the operands and the
 // accumulators live?  (tools/probe_mfma_order.hip measured ≈ 27 cycles per MFMA for ONE
 // wave per SIMD with the B operand in AGPRs, ≈ 13.8 for two waves with VGPR operands.)
-// Independent accumulators, operands in registers, asm MFMAs, 256 workgroups:
+// Independent accumulators, operands in registers, asm MFMAs, 256 workgroups; time = the
+// workgroup's slowest wave, stamped after its accumulators are consumed:
 //   V1    1 wave / SIMD: A, B in VGPRs, 8 accumulators in VGPRs
 //   V1A   1 wave / SIMD: A, B in VGPRs, 8 accumulators in AGPRs
 //   V1B   1 wave / SIMD: src0 (the weight fragment) in AGPRs (the k_gemm_wsa shape)
@@ -46,18 +47,19 @@ __global__ void k(int rounds, const v4i* rnd, int* sink, unsigned long long* out
       for (int i = 0; i < NACC; ++i) mf<MODE>(acc[i], w[(s + i) & 7], a[i & 1]);
   }
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory");
-  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   int s = 0;
 #pragma unroll
   for (int i = 0; i < NACC; ++i) s ^= acc[i][0] ^ acc[i][3];
+  asm volatile("" ::"v"(s));                     // the stream has retired before the stamp
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   if (s == 0x1234567) sink[tid] = s;
-  if (tid == 0) out[blockIdx.x] = t1 - t0;
+  if ((tid & 63) == 0) out[blockIdx.x * 8 + (tid >> 6)] = t1 - t0;   // every wave
 }
 
 int main() {
   const int grid = 256, rounds = 400;
   unsigned long long* d; int* sink; v4i* rnd;
-  hipMalloc(&d, grid * 8); hipMalloc(&sink, 4096 * 4);
+  hipMalloc(&d, grid * 8 * 8); hipMalloc(&sink, 4096 * 4);
   const size_t nr = 512 * 256 * 16;
   hipMalloc(&rnd, nr * 16);
   {
@@ -77,12 +79,17 @@ int main() {
       {"V2    2 waves/SIMD, VGPR operands, 8 VGPR accumulators", 512, 8, k<0, 8>},
   };
   for (const M& m : modes) {
+    hipMemset(d, 0, grid * 8 * 8);
     for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(m.f, dim3(grid), dim3(m.threads), 0, 0, rounds, rnd, sink, d);
     hipDeviceSynchronize();
-    unsigned long long h[256];
-    hipMemcpy(h, d, grid * 8, hipMemcpyDeviceToHost);
-    double c = 0;
-    for (int i = 0; i < grid; ++i) c += h[i];
+    unsigned long long h[256 * 8];
+    hipMemcpy(h, d, grid * 8 * 8, hipMemcpyDeviceToHost);
+    double c = 0;                                  // the workgroup's slowest wave
+    for (int i = 0; i < grid; ++i) {
+      unsigned long long mx = 0;
+      for (int w = 0; w < 8; ++w) mx = h[i * 8 + w] > mx ? h[i * 8 + w] : mx;
+      c += mx;
+    }
     c /= grid;
     const double per_simd = (double)rounds * 8 * m.nacc * (m.threads / 256);   // MFMAs per SIMD
     printf("%s: %.1f cycles per MFMA per SIMD\n", m.name, c / per_simd);
