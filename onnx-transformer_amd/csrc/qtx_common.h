@@ -262,6 +262,23 @@ __device__ __forceinline__ float quant_scale(float absmax, float qmax) {
   return div_const(fmaxf(absmax, 1e-5f), qmax);
 }
 __device__ __forceinline__ int quant_val(float x, float s) { return (int)rintf(x / s); }
+// Branch-free short forms of the scale chain for a >= 1e-5 (a row's clamped absmax), each
+// equal to the IEEE operation on every such input — checked exhaustively on the GPU's own
+// v_rcp_f32 (tools/probe_scale_exact.hip, profiles/r04_scale_exact.log):
+//   scale127(a) = RN(a / 127): div_cr with the folded reciprocal, a scaled by 2^-64 when
+//                 a >= 2^60 (exact power-of-two scaling), +inf passed through
+//   rcp_cr(s)   = RN(1 / s) for s >= 1e-5 / 127: one Newton step with fma from v_rcp_f32,
+//                 1 / +inf = 0
+__device__ __forceinline__ float scale127(float a) {
+  const bool big = a >= 0x1p60f;
+  const float q = div_cr(big ? a * 0x1p-64f : a, 127.0f, 1.0f / 127.0f);
+  return a == __builtin_inff() ? a : (big ? q * 0x1p64f : q);
+}
+__device__ __forceinline__ float rcp_cr(float s) {
+  const float y0 = __builtin_amdgcn_rcpf(s);
+  const float y = fmaf(fmaf(-s, y0, 1.0f), y0, y0);
+  return s == __builtin_inff() ? 0.0f : y;
+}
 
 // pack 4 ints (already in [-127,127]) into one dword of int8
 __device__ __forceinline__ uint32_t pack4_i8(int a, int b, int c, int d) {
