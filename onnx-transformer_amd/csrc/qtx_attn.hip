@@ -391,7 +391,7 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
     // P = rint((e / den) * 127) / 127 with both divisions by div_cr, unguarded: den is in
     // [1, 128] (the row max contributes qexp(0) == 1), so e / den is correctly rounded for
     // every e >= 2^-60, and e < 2^-60 (or 0) gives P == 0 through either quotient
-    const float rden = 1.0f / den;
+    const float rden = rcp_cr(den);       // RN(1 / den), den in [1, 128] (qtx_common.h)
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
@@ -546,8 +546,8 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) am = fmaxf(am, fabsf(ctx[h][dt][e]));
     am = row16_max(am);
-    sc[e] = quant_scale(am, 127.0f);
-    inv[e] = 1.0f / sc[e];
+    sc[e] = scale127(fmaxf(am, 1e-5f));   // quant_scale(am, 127) and 1 / s, branch-free
+    inv[e] = rcp_cr(sc[e]);
     big |= !(am < 0x1p37f);
   }
   auto store_rows = [&](auto quot) {
