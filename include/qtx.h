@@ -49,8 +49,8 @@ typedef enum {
   QTX_E_UNSUPPORTED = 4,
   QTX_E_DEVICE = 5     /* a kernel flagged an error it cannot repair in the calling
                         * thread's device status word on the model (k_gemm_wsx: FFN1 row-max
-                        * exchange timed out, outputs invalid); reported by qtx_model_check
-                        * (the thread's next model-level call on the model zeroes the word) */
+                        * exchange timed out, outputs invalid); reported (and cleared) by
+                        * qtx_model_check — no later call clears it before that */
 } qtx_status;
 
 typedef struct qtx_model qtx_model;
@@ -119,9 +119,13 @@ int32_t qtx_greedy_decode(const qtx_model* m, const int64_t* src, const uint8_t*
                           void* ws, size_t ws_bytes, void* stream);
 
 /* Synchronise `stream`, then report (and clear) the calling thread's device status word on
- * this model: QTX_OK, or QTX_E_DEVICE if a kernel of the thread's last model-level call on it
- * flagged an error (the outputs of that call are invalid; every model-level call zeroes the
- * word first).  The Python layer calls it wherever it synchronises anyway. */
+ * this model: QTX_OK, or QTX_E_DEVICE if a kernel of any of the thread's model-level calls on
+ * it since its last check raised an error (the bits accumulate; nothing but this check clears
+ * them).  Thread affinity: the word belongs to the thread that made the calls, so check from
+ * that thread; a thread that made no encoder / greedy-decode call on the model gets QTX_OK.
+ * A thread claims its word at its first encoder / greedy-decode call on the model and returns
+ * it when it exits; at most 256 threads may hold one per model at a time — the call of a
+ * further thread fails with QTX_E_UNSUPPORTED instead of sharing a word. */
 int32_t qtx_model_check(const qtx_model* m, void* stream);
 
 /* ---- fault injection (the reference's campaigns: inject_utils/layers.py:48-84,

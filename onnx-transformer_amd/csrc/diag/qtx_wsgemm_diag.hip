@@ -6,8 +6,8 @@
 #include <cstdlib>
 #include <type_traits>
 
-#include "qtx_knobs.h"
-#include "qtx_ws.h"
+#include "../qtx_knobs.h"
+#include "../qtx_ws.h"
 
 namespace qtx {
 

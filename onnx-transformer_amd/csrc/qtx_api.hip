@@ -124,7 +124,8 @@ struct qtx_model {
   int device = 0;            // the device the model's memory lives on
   unsigned long long serial = 0;   // unique per created model (call status records)
   unsigned* status = nullptr;      // kStatusSlots 16-byte status words (model memory)
-  std::atomic<int> next_status{0};
+  std::mutex slot_mu;              // guards slot_used
+  std::vector<bool> slot_used;     // a live thread holds the slot (qtx_api.hip CallStatus)
   // an exec may still be running on a caller's stream: wait for its last replay first
   void clear_graphs() {
     for (auto& kv : graphs) {
@@ -162,39 +163,91 @@ const char* status_text(unsigned v) {
                "FFN hidden was quantized from a partial row maximum): outputs invalid"
              : "device status word set";
 }
-// Status words live in the model's own memory: kStatusSlots 16-byte words, one per calling
-// thread (a thread's first model-level call on a model claims the next slot; past
-// kStatusSlots threads, slots are shared round robin).  Every model-level call zeroes its
-// thread's word on its stream before its kernels run; a kernel that detects an error it
-// cannot repair (k_gemm_wsy's exchange timeout) ORs a DEV_E_* bit into it.
+// Status words live in the model's own memory: kStatusSlots 16-byte words, one per live
+// calling thread.  A thread's first model-level call that can raise a device error (the
+// encoder and greedy-decode entry points) claims a free slot and zeroes it on its stream;
+// the slot returns to the model when the thread exits.  A kernel that detects an error it
+// cannot repair (k_gemm_wsy's exchange timeout) ORs a DEV_E_* bit into the word, and the bit
+// stays until qtx_model_check reports it (later calls never clear it: ADVICE r04).
 // qtx_model_check(m, stream) synchronises the stream and reads the calling thread's word,
 // so an error is reported to the thread whose call raised it and no other thread's call can
 // clear it, and no later use of a caller's workspace can overwrite it.
-constexpr int kStatusSlots = 64;
+// No slot is ever shared: a thread that finds every slot held by a live thread gets
+// QTX_E_UNSUPPORTED (VERDICT r04 hygiene; QTX_STATUS_SLOTS lowers the cap for the test).
+constexpr int kStatusSlots = 256;
 struct CallStatus {
   const qtx_model* m = nullptr;
   unsigned long long serial = 0;    // the model's creation serial (a new model at a freed
-  unsigned* word = nullptr;         // address is a different model)
+  int slot = -1;                    // address is a different model)
 };
-constexpr int kCallSlots = 32;     // models a thread keeps its word for (round robin past it:
-                                   // the next call on an evicted model claims a new word)
-thread_local CallStatus t_calls[kCallSlots];
-thread_local int t_next = 0;
+// live models by serial: a thread's exit returns its slots only to models still alive
+std::mutex g_live_mu;
+std::map<unsigned long long, qtx_model*> g_live;
+void release_slot(const CallStatus& c);
+struct ThreadCalls {
+  std::vector<CallStatus> v;
+  ~ThreadCalls() {
+    for (const CallStatus& c : v) release_slot(c);
+  }
+};
+thread_local ThreadCalls t_calls;
 
-unsigned* thread_status_word(qtx_model* m) {
-  for (CallStatus& c : t_calls)
-    if (c.m == m && c.serial == m->serial) return c.word;
-  unsigned* w = m->status + 4 * (m->next_status.fetch_add(1) % kStatusSlots);
-  t_calls[t_next] = CallStatus{m, m->serial, w};
-  t_next = (t_next + 1) % kCallSlots;
-  return w;
+int status_slot_cap() {
+  const int n = knobs().status_slots;
+  return n > 0 && n < kStatusSlots ? n : kStatusSlots;
 }
 
-// the calling thread's word, zeroed on st (a kernel: graph-capturable, stream-ordered)
+// the calling thread's word for m (nullptr: every slot is held by a live thread); *fresh is
+// set when the slot was claimed by this call (its word must be zeroed)
+unsigned* thread_status_word(qtx_model* m, bool* fresh) {
+  *fresh = false;
+  for (const CallStatus& c : t_calls.v)
+    if (c.m == m && c.serial == m->serial) return m->status + 4 * c.slot;
+  int slot = -1;
+  {
+    std::lock_guard<std::mutex> lk(m->slot_mu);
+    const int cap = status_slot_cap();
+    for (int i = 0; i < cap; ++i)
+      if (!m->slot_used[i]) { m->slot_used[i] = true; slot = i; break; }
+  }
+  if (slot < 0) return nullptr;
+  // drop the records of models destroyed since (their serials are gone from g_live)
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    auto& v = t_calls.v;
+    v.erase(std::remove_if(v.begin(), v.end(),
+                           [](const CallStatus& c) {
+                             auto it = g_live.find(c.serial);
+                             return it == g_live.end() || it->second != c.m;
+                           }),
+            v.end());
+  }
+  t_calls.v.push_back(CallStatus{m, m->serial, slot});
+  *fresh = true;
+  return m->status + 4 * slot;
+}
+
+void release_slot(const CallStatus& c) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  auto it = g_live.find(c.serial);
+  if (it == g_live.end() || it->second != c.m) return;   // the model is gone
+  qtx_model* m = it->second;
+  std::lock_guard<std::mutex> lk2(m->slot_mu);
+  m->slot_used[c.slot] = false;
+}
+
+// the calling thread's word (claimed and zeroed on st by its first call: a kernel,
+// graph-capturable and stream-ordered)
 int call_status_begin(const qtx_model* mc, unsigned** word, hipStream_t st) {
   qtx_model* m = const_cast<qtx_model*>(mc);
-  *word = thread_status_word(m);
-  HIPCHK(launch_zero(*word, 16, st));
+  bool fresh = false;
+  *word = thread_status_word(m, &fresh);
+  if (!*word)
+    return fail(QTX_E_UNSUPPORTED,
+                "every device status word of this model is held by a live thread (%d): "
+                "at most that many threads may call one model at a time",
+                status_slot_cap());
+  if (fresh) HIPCHK(launch_zero(*word, 16, st));
   return QTX_OK;
 }
 
@@ -307,6 +360,11 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
   qtx_model* m = new qtx_model();
   static std::atomic<unsigned long long> next_serial{1};
   m->serial = next_serial.fetch_add(1);
+  m->slot_used.assign(kStatusSlots, false);
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live[m->serial] = m;
+  }
   m->cfg = c;
   (void)hipGetDevice(&m->device);
   Arena sizing;
@@ -403,6 +461,10 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
 
 int32_t qtx_model_destroy(qtx_model* m) {
   if (!m) return QTX_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);   // no thread exit returns a slot to it now
+    g_live.erase(m->serial);
+  }
   for (hipStream_t s : m->gstream)
     if (s) (void)hipStreamSynchronize(s);
   m->clear_graphs();
@@ -1318,12 +1380,12 @@ int32_t qtx_decoder_forward_fault(const qtx_model* m, const float* y, const floa
   hipStream_t st = (hipStream_t)stream;
   const qtx_config& c = m->cfg;
   const int D = c.d_model, M = B * T;
-  unsigned* cst = nullptr;
-  RC(call_status_begin(m, &cst, st));
+  // no decoder kernel sets a status word (the in-launch FFN1 exchange runs on the KP
+  // encoder path only), so this call neither claims nor touches the thread's word: an
+  // error an earlier encode left there stays until qtx_model_check reports it
   Arena ar;
   ar.base = (uint8_t*)ws; ar.cap = ws_bytes;
   Scratch s = carve_scratch(ar, c, M);
-  s.status = cst;
   CrossKV x = carve_cross(ar, c, (long)B * S);
   RC(cross_kv(m, memory, B * S, x, st, f));
   HIPCHK(hipMemcpyAsync(s.x, y, (size_t)M * D * 4, hipMemcpyDeviceToDevice, st));
@@ -1453,9 +1515,11 @@ int32_t qtx_model_check(const qtx_model* m, void* stream) {
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   unsigned v = 0;
   unsigned* word = nullptr;
-  for (const CallStatus& cs : t_calls)
-    if (cs.m == m && cs.serial == m->serial) word = cs.word;
-  if (!word) return QTX_OK;                 // no model-level call on this thread yet
+  for (const CallStatus& cs : t_calls.v)
+    if (cs.m == m && cs.serial == m->serial) word = m->status + 4 * cs.slot;
+  // no word: this thread has made no call on m that can raise a device error (the word is
+  // per thread: a check reports the calling thread's calls only)
+  if (!word) return QTX_OK;
   HIPCHK(hipMemcpy(&v, word, sizeof v, hipMemcpyDeviceToHost));
   if (!v) return QTX_OK;
   HIPCHK(hipMemset(word, 0, sizeof(unsigned)));   // reported once (the thread's own word)
@@ -1546,9 +1610,10 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
   const bool joint = gr.G > 1 && knobs().group_graph;
   // the switches a captured step depends on are part of its key (knobs can be reloaded)
   const Knobs& kn = knobs();
-  const std::string variant = std::to_string(kn.split_ln) + std::to_string(kn.ffn_qkernel) + ":" +
-                              std::to_string(kn.ablate) + std::to_string(kn.ablate_nop) +
-                              std::to_string(kn.group_graph);
+  // (every switch: the key carries the knob generation, bumped by each reload — ADVICE r04:
+  // QTX_SKINNY_WIDE, QTX_RB_*, ... pick launch shapes inside the captured step too)
+  const std::string variant = std::to_string(knobs_generation()) + ":" + std::to_string(kn.split_ln) +
+                              std::to_string(kn.ffn_qkernel) + std::to_string(kn.group_graph);
   const GraphKey key{B, S, max_len, gr.G * 1000 + per_graph, g.gsteps, variant};
   auto it = mm->graphs.find(key);
   if (it == mm->graphs.end()) {

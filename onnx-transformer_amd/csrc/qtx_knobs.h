@@ -33,6 +33,8 @@ struct Knobs {
   long ws_min_m = 2048;      // QTX_WS_MIN_M: weight-stationary from this many rows
   long ws_res_min_m = 2048;  // QTX_WS_RES_MIN_M / _MAX_M: the O-projection's WS range
   long ws_res_max_m = 8192;
+  int status_slots = 0;      // QTX_STATUS_SLOTS: device status words per model (0: all 256;
+                             // tests lower it to make exhaustion happen)
   // ---- hooks of the FFN1 exchange's error path (tests/test_gpu_status.py)
   int wsx_spin_limit = -1;   // QTX_WSX_SPIN_LIMIT: polls per wait (-1: the launcher's bound)
   int wsx_drop_slice = -1;   // QTX_WSX_DROP_SLICE: this column slice never publishes its
@@ -60,5 +62,8 @@ struct Knobs {
 const Knobs& knobs();
 // re-read them (tests; not thread-safe against concurrent launches)
 void knobs_reload();
+// how many reloads so far: part of every cached decode graph's key, so a graph captured
+// under other switches is never replayed after a reload
+int knobs_generation();
 
 }  // namespace qtx

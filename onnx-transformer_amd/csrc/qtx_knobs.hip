@@ -1,6 +1,7 @@
 // qtx_knobs.hip — reads the environment switches of qtx_knobs.h once.
 #include "qtx_knobs.h"
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -40,6 +41,7 @@ Knobs read_env() {
   k.ws_min_m = num("QTX_WS_MIN_M", 2048L);
   k.ws_res_min_m = num("QTX_WS_RES_MIN_M", 2048L);
   k.ws_res_max_m = num("QTX_WS_RES_MAX_M", 8192L);
+  k.status_slots = (int)num("QTX_STATUS_SLOTS", 0);
   k.wsx_spin_limit = (int)num("QTX_WSX_SPIN_LIMIT", -1);
   k.wsx_drop_slice = (int)num("QTX_WSX_DROP_SLICE", -1);
 #ifdef QTX_DIAG
@@ -68,6 +70,7 @@ Knobs read_env() {
 
 Knobs g_knobs;
 std::once_flag g_once;
+std::atomic<int> g_generation{0};
 
 }  // namespace
 
@@ -78,7 +81,9 @@ const Knobs& knobs() {
 void knobs_reload() {
   knobs();
   g_knobs = read_env();
+  g_generation.fetch_add(1);
 }
+int knobs_generation() { return g_generation.load(); }
 
 }  // namespace qtx
 

@@ -17,7 +17,7 @@ SOURCES = ["qtx_kernels.hip", "qtx_decode.hip", "qtx_gemm.hip", "qtx_wsgemm.hip"
            "qtx_api.hip", "qtx_knobs.hip"]
 # measured-negative kernel variants and their switches: compiled only into the diagnostic
 # library (build(extra=...) -> libqtx_diag.so, with -DQTX_DIAG), never into libqtx.so
-DIAG_SOURCES = ["qtx_wsgemm_diag.hip"]
+DIAG_SOURCES = ["diag/qtx_wsgemm_diag.hip"]   # csrc/diag/: outside the product sources
 HEADERS = ["qtx_common.h", "qtx_kernels.h", "qtx_ws.h", "qtx_knobs.h"]
 
 # -ffp-contract=off: every float op is a separate IEEE op (the numerics contract,
@@ -61,7 +61,7 @@ def build(force: bool = False, verbose: bool = False, extra=()) -> str:
     cflags = [f for f in FLAGS if f != "-shared"] + list(extra)
 
     def compile_one(src):
-        obj = os.path.join(objdir, os.path.splitext(src)[0] + ("_x" if extra else "") + ".o")
+        obj = os.path.join(objdir, os.path.splitext(os.path.basename(src))[0] + ("_x" if extra else "") + ".o")
         cmd = [hipcc(), *cflags, "-c", "-o", obj, os.path.join(CSRC, src)]
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -50,6 +50,7 @@ def greedy_decode_fault(model: QtxModel, src, src_mask, max_len: int, start_symb
         model.check()
         return ys.cpu().numpy()
     memory = model.encode(model.embed(srcd, "src"), md)
+    model.check()                               # the encode's device errors, before the loop
     ys = torch.full((B, 1), int(start_symbol), dtype=torch.int64, device=dev)
     for i in range(max_len - 1):
         T = ys.shape[1]

@@ -91,7 +91,7 @@ def test_ws_kernels_wait_vmcnt_zero():
 
 def test_product_sources_read_no_environment_per_launch():
     """Product hygiene: kernels and launchers read their switches through qtx_knobs.h (once),
-    never getenv() per launch; measured-negative variants live in qtx_wsgemm_diag.hip, which
+    never getenv() per launch; measured-negative variants live in csrc/diag/qtx_wsgemm_diag.hip, which
     only the diagnostic build compiles."""
     sys.path.insert(0, os.path.join(REPO, "onnx-transformer_amd"))
     from qtx import _build
@@ -100,4 +100,5 @@ def test_product_sources_read_no_environment_per_launch():
         if f == "qtx_knobs.hip":
             continue
         assert "getenv(" not in code, f"{f} reads the environment outside qtx_knobs"
-    assert "qtx_wsgemm_diag.hip" not in _build.SOURCES
+    assert not any("diag" in f for f in _build.SOURCES)
+    assert all(f.startswith("diag/") for f in _build.DIAG_SOURCES)

@@ -195,3 +195,70 @@ def test_workspace_reuse_reports_no_false_error(torch, gpu_model):
     gpu_model.check()
     gpu_model.encode(x, m)
     gpu_model.check()
+
+
+def test_decoder_call_keeps_encode_error(torch, gpu_model, knob_env):
+    """a decoder call after an encode whose FFN1 exchange timed out must
+    not erase that error before the check (the greedy_decode_fault loop: encode, then decoder
+    calls, then one check).  B = 32, S = 72 (M = 2304): the encode runs the one-pass FFN1."""
+    from qtx._lib import QtxError
+    knob_env("QTX_WSX_SPIN_LIMIT", 64)
+    knob_env("QTX_WSX_DROP_SLICE", 1)
+    x = torch.randn((32, 72, 512), device="cuda")
+    m = torch.ones((32, 72), dtype=torch.uint8, device="cuda")
+    mem = gpu_model.encode(x, m)
+    knob_env("QTX_WSX_DROP_SLICE", -1)
+    y = torch.randn((32, 5, 512), device="cuda")
+    tm = torch.tril(torch.ones((5, 5), dtype=torch.uint8, device="cuda"))
+    gpu_model.decode(y, mem, m, tm)
+    gpu_model.decode(y, mem, m, tm)
+    with pytest.raises(QtxError) as e:
+        gpu_model.check()
+    assert e.value.code == 5
+    gpu_model.check()                                  # reported once, then cleared
+
+
+def test_status_slots_exhaustion_is_loud(torch, state_dict, knob_env):
+    """VERDICT r04 hygiene: status words are never shared.  With the cap lowered to 4
+    (QTX_STATUS_SLOTS), 4 live threads hold a word each and a 5th thread's encode fails with
+    QTX_E_UNSUPPORTED; once those threads exit their words return to the model, and 12
+    short-lived threads in turn all run clean."""
+    import threading
+    from qtx._lib import QtxError
+    from qtx.model import QtxModel
+    knob_env("QTX_STATUS_SLOTS", 4)
+    model = QtxModel(state_dict)                       # fresh slots
+    x = torch.randn((2, 8, 512), device="cuda")
+    m = torch.ones((2, 8), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    hold, res = threading.Event(), {}
+
+    def worker(name, wait):
+        try:
+            model.encode(x, m)
+            model.check()
+            res[name] = "ok"
+        except QtxError as e:
+            res[name] = e.code
+        if wait:
+            hold.wait(timeout=60)
+    live = [threading.Thread(target=worker, args=(f"h{i}", True)) for i in range(4)]
+    for t in live:
+        t.start()
+    import time
+    t0 = time.time()
+    while len(res) < 4 and time.time() - t0 < 60:
+        time.sleep(0.01)
+    extra = threading.Thread(target=worker, args=("extra", False))
+    extra.start()
+    extra.join(timeout=60)
+    hold.set()
+    for t in live:
+        t.join(timeout=60)
+    assert res == {**{f"h{i}": "ok" for i in range(4)}, "extra": 4}, res
+    res.clear()
+    for i in range(12):
+        t = threading.Thread(target=worker, args=(f"s{i}", False))
+        t.start()
+        t.join(timeout=60)
+    assert res == {f"s{i}": "ok" for i in range(12)}, res

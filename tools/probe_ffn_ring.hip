@@ -1,0 +1,190 @@
+// probe_ffn_ring.hip — diagnostic (not shipped): the L2 -> LDS weight stream of the fused FFN
+// row-block kernel (VERDICT r04 "next round" item 1, step 1), measured as a skeleton with the
+// MFMAs the kernel issues and no epilogue arithmetic.
+//
+// One 128-row block per CU (cfg3: M = 32768 = 256 blocks).  The block's weights arrive as one
+// linear stream of 32 KB slots in MFMA-fragment order (1 KB = one 16 x 64 fragment, lane l's
+// 16 bytes at 16 l), so a slot is filled by 32 linear 1 KB LDS-DMA pieces and read by linear
+// ds_read_b128 (conflict-free):
+//   pass 1 (FFN1 row maxima):   32 W1 slots,                      64 MFMAs per wave each
+//   pass 2 (FFN1 + FFN2):        32 x (W1 slot, W2 K-step slot),   64 MFMAs per wave each
+// = 96 slots = 3 MB per CU.  Every wave reads every byte of every slot (its own rows).
+// Ring: NSLOT slots, per slot each wave waits for its own pieces (counted vmcnt: the loop
+// holds no other memory operation), one s_barrier, then issues slot s + NSLOT - 1 into the
+// slot consumed at s - 1.
+// Variants: waves per workgroup (4 = one per SIMD, the 512-register design; 8 = two per SIMD,
+// rows split), ring depth, per-CU rotation of the mini-chunk order (exact in the kernel: int32
+// sums and maxima are order-free; CUs of one XCD then do not request the same W lines at the
+// same time), nt policy on the weight pieces, and the fill alone / the consumers alone.
+//   hipcc --offload-arch=gfx950 -O3 -o tools/probe_ffn_ring tools/probe_ffn_ring.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+constexpr int SLOT = 32 * 1024;
+constexpr int NCHUNK = 32;                 // 64-column FFN1 mini-chunks (d_ff 2048)
+constexpr int NSTREAM = 3 * NCHUNK;        // slots consumed per block
+
+template <bool NT>
+__device__ __forceinline__ void dma16(const int8_t* gsrc, const uint8_t* lds_dst) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+  unsigned keep;
+  if constexpr (NT)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+}
+
+// MODE 0: fill + consume; 1: fill only; 2: consume only (no DMA)
+template <int NW, int NSLOT, bool ROT, bool NT, int MODE, int PD = 0>
+__global__ __launch_bounds__(NW * 64) void k_ring(const int8_t* W, int* sink, unsigned long long* out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NSLOT * SLOT];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  constexpr int PPW = 32 / NW;               // 1 KB pieces per wave per slot
+  // pass 2's stream is (W1 chunk c, W2 K-step c) interleaved: slot 2c and 2c + 1 of a 2 MB
+  // region; pass 1 reads the W1 slots of it
+  const int rot = ROT ? (int)((blockIdx.x >> 3) * 5 + (blockIdx.x & 7) * 3) % NCHUNK : 0;
+  auto src_slot = [&](int j) {               // stream position j -> slot index in W
+    const int pass2 = j >= NCHUNK;
+    const int c0 = pass2 ? (j - NCHUNK) >> 1 : j;
+    const int c = (c0 + rot) % NCHUNK;
+    return pass2 ? 2 * c + ((j - NCHUNK) & 1) : 2 * c;
+  };
+  auto issue = [&](int j) {
+    if (MODE == 2 || j >= NSTREAM) return;
+    const int8_t* src = W + (long)src_slot(j) * SLOT + (wave * PPW) * 1024 + lane * 16;
+    uint8_t* dst = lds + (j % NSLOT) * SLOT + (wave * PPW) * 1024;
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) dma16<NT>(src + p * 1024, dst + p * 1024);
+  };
+  // operands held in registers by the kernel: the block's x1q rows (4 waves: 2 row
+  // fragments x 8 K steps; 8 waves: 1 x 8) and FFN2's hq fragments
+  constexpr int RF = NW == 4 ? 2 : 1;
+  v4i xa[RF][8];
+#pragma unroll
+  for (int i = 0; i < RF; ++i)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) xa[i][s] = v4i{tid + i, s, lane * 3, i ^ s};
+  v4i acc[RF][8];
+#pragma unroll
+  for (int i = 0; i < RF; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+  for (int j = 0; j < NSLOT - 1; ++j) issue(j);
+  __syncthreads();
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (int s = 0; s < NSTREAM; ++s) {
+    if (MODE != 2) {
+      // this wave's pieces of slot s landed: the youngest are slots s+1 .. s+NSLOT-2
+      const int ahead = min(NSLOT - 2, NSTREAM - 1 - s);
+      if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPW) : "memory");
+      else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(s + NSLOT - 1);
+    if (MODE == 1) continue;
+    const uint8_t* slot = lds + (s % NSLOT) * SLOT;
+    if constexpr (PD == 0) {
+      // 32 fragments per slot; each consumed by RF row fragments (2 MFMAs per fragment at
+      // 4 waves: 64 per slot per wave)
+#pragma unroll 4
+      for (int f = 0; f < 32; f += 4) {
+        v4i b[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const v4i*>(slot + (f + q) * 1024 + lane * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int i = 0; i < RF; ++i)
+            acc[i][(f + q) & 7] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[q], xa[i][(f + q) & 7], acc[i][(f + q) & 7], 0, 0, 0);
+      }
+    } else {
+      // software-pipelined: the fragment PD ahead is read while this one is multiplied
+      v4i b[PD];
+#pragma unroll
+      for (int q = 0; q < PD; ++q) b[q] = *reinterpret_cast<const v4i*>(slot + q * 1024 + lane * 16);
+#pragma unroll
+      for (int f = 0; f < 32; ++f) {
+        const v4i cur = b[f % PD];
+        if (f + PD < 32) b[f % PD] = *reinterpret_cast<const v4i*>(slot + (f + PD) * 1024 + lane * 16);
+#pragma unroll
+        for (int i = 0; i < RF; ++i)
+          acc[i][f & 7] = __builtin_amdgcn_mfma_i32_16x16x64_i8(cur, xa[i][f & 7], acc[i][f & 7], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int sum = 0;
+#pragma unroll
+  for (int i = 0; i < RF; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum += acc[i][j][0] ^ acc[i][j][3];
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (sum == 0x1234567) sink[tid] = sum;
+  if (tid == 0) { out[blockIdx.x * 2] = t1 - t0; out[blockIdx.x * 2 + 1] = r1 - r0; }
+}
+
+typedef void (*KFn)(const int8_t*, int*, unsigned long long*);
+struct Var { const char* name; KFn f; int threads; int mode; };
+
+int main() {
+  int ncu = 0;
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+  const long wbytes = 2L * NCHUNK * SLOT;           // the 2 MB stream region (3 MB read per CU)
+  int8_t* W; int* sink; unsigned long long* d;
+  hipMalloc(&W, wbytes); hipMalloc(&sink, 4096); hipMalloc(&d, 4096 * 16);
+  {
+    int8_t* h = (int8_t*)malloc(wbytes);
+    unsigned x = 7;
+    for (long i = 0; i < wbytes; ++i) { x = x * 1664525u + 1013904223u; h[i] = (int8_t)(x >> 24); }
+    hipMemcpy(W, h, wbytes, hipMemcpyHostToDevice);
+    free(h);
+  }
+  Var vars[] = {
+      {"4w 4slot rotated          ", k_ring<4, 4, true, false, 0>, 256, 0},
+      {"4w consume-only           ", k_ring<4, 4, true, false, 2>, 256, 2},
+      {"4w 4slot rotated pd4      ", k_ring<4, 4, true, false, 0, 4>, 256, 0},
+      {"4w consume-only pd4       ", k_ring<4, 4, true, false, 2, 4>, 256, 2},
+      {"4w 4slot rotated pd8      ", k_ring<4, 4, true, false, 0, 8>, 256, 0},
+      {"4w consume-only pd8       ", k_ring<4, 4, true, false, 2, 8>, 256, 2},
+      {"4w 4slot rotated pd16     ", k_ring<4, 4, true, false, 0, 16>, 256, 0},
+      {"4w consume-only pd16      ", k_ring<4, 4, true, false, 2, 16>, 256, 2},
+      {"4w 5slot rotated pd8      ", k_ring<4, 5, true, false, 0, 8>, 256, 0},
+      {"4w 3slot rotated pd8      ", k_ring<4, 3, true, false, 0, 8>, 256, 0},
+      {"4w 4slot rotated pd8 nt   ", k_ring<4, 4, true, true, 0, 8>, 256, 0},
+      {"8w 4slot rotated pd4      ", k_ring<8, 4, true, false, 0, 4>, 512, 0},
+      {"8w consume-only pd4       ", k_ring<8, 4, true, false, 2, 4>, 512, 2},
+  };
+  printf("CUs %d; per CU %.2f MB streamed (96 x 32 KB slots); MFMA floor at 4 waves = 96 x 64 x 16 cycles\n",
+         ncu, 3.0 * NCHUNK * SLOT / 1048576.0);
+  for (int rep = 0; rep < 2; ++rep)
+    for (const Var& v : vars) {
+      auto launch = [&]() { v.f<<<ncu, v.threads>>>(W, sink, d); };
+      for (int w = 0; w < 3; ++w) launch();
+      hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+      hipEventRecord(e0);
+      const int reps = 20;
+      for (int w = 0; w < reps; ++w) launch();
+      hipEventRecord(e1); hipEventSynchronize(e1);
+      float ms; hipEventElapsedTime(&ms, e0, e1);
+      unsigned long long h[2 * 1024];
+      hipMemcpy(h, d, ncu * 16, hipMemcpyDeviceToHost);
+      double ticks = 0, real = 0;
+      for (int b = 0; b < ncu; ++b) { ticks += h[2 * b]; real += h[2 * b + 1]; }
+      ticks /= ncu; real /= ncu;
+      const double us = ms / reps * 1e3;
+      const double bytes_cu = v.mode == 2 ? 0.0 : (double)NSTREAM * SLOT;
+      printf("%s: %6.1f us per launch (in-kernel %6.1f us, clock %4.0f MHz, %6.0f cycles), fill %5.1f GB/s per CU\n",
+             v.name, us, real / 100.0, ticks / (real / 100.0), ticks, bytes_cu / (real / 100.0 * 1e-6) / 1e9);
+      hipEventDestroy(e0); hipEventDestroy(e1);
+    }
+  return 0;
+}
