@@ -292,6 +292,30 @@ typedef struct qtx_row_gemm {
   int32_t ksplit;
 } qtx_row_gemm;
 int32_t qtx_linear_rows(const qtx_row_gemm* args, void* stream);
+/* The encoder's FFN sublayer as ONE launch (position_feed_forward.py:11-12 with its
+ * sublayer_connection.py:15-17 residual and the next layer_norm.py:12-15 + quant_linear.py:30-43),
+ * replacing the FFN1 (qtx_linear_rows kp = 3) and FFN2 (kp = 1, epi 1) calls:
+ *   h = relu(((float(A . W1^T) * sa) * sw1) + b1) quantized per token over all F columns,
+ *   x = x + (((float(hq . W2^T) * s_h) * sw2) + b2)   (in place),
+ *   LayerNorm(x; ln_a, ln_b) quantized per token -> lnq (KP) + lns [M], or fp32 -> lnout when
+ *   lnq is NULL.  A: int8 [M (+1 if odd), 512] in the KP layout (qtx_linear_rows kp = 1);
+ *   wf: W1 / W2 packed by qtx_pack_ffn.  lnq / lns may alias A / sa (each 128-row block reads
+ *   its rows before it writes them).  F % 64 == 0, 256 <= F <= 2048.  Results equal the two
+ *   calls it replaces bit for bit. */
+typedef struct qtx_ffn_args {
+  const int8_t* A; const float* sa; const int8_t* wf;
+  const float* sw1; const float* b1; const float* sw2; const float* b2;
+  float* x; const float* ln_a; const float* ln_b;
+  int8_t* lnq; float* lns; float* lnout;
+  int32_t M, F;
+} qtx_ffn_args;
+int32_t qtx_ffn_rows(const qtx_ffn_args* args, void* stream);
+/* W1 int8 [F, 512] and W2 int8 [512, F] row-major -> the weight stream qtx_ffn_rows reads
+ * (F * 1024 bytes): per 64-column chunk c a 32 KB W1 slot (fragment 4s + j', lane l: W1[64c +
+ * 16j' + (l & 15)][64s + 16(l >> 4) .. +16]) and a 32 KB W2 slot (fragment j, lane l: byte
+ * 4j' + e = W2[col][64c + 16j' + 4(l >> 4) + e], col = 16(l & 15) + j for j < 16, else
+ * 256 + 16(l & 15) + j - 16). */
+int32_t qtx_pack_ffn(const int8_t* W1, const int8_t* W2, int32_t F, int8_t* out, void* stream);
 /* W int8 [N, K] row-major -> out [N, K] in the KP layout with the per-512-column-tile row
  * order qtx_linear_rows(kp = 1) reads.  N % 512 == 0, K % 64 == 0. */
 int32_t qtx_pack_w_kp(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* stream);

@@ -77,6 +77,7 @@ struct QLin {
 struct EncLayer {
   QLin qkv, o, w1, w2;
   const float* ln[2][2];
+  int8_t* ffn = nullptr;   // W1 + W2 as k_ffn_fused's weight stream (launch_pack_ffn)
 };
 struct DecLayer {
   QLin qkv, o, cq, ckv, co, w1, w2;
@@ -342,6 +343,8 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     if (c.d_ff % 512 == 0)   // weight-stationary copies (K = 512 GEMMs)
       for (auto& e : m->enc)
         for (QLin* L : {&e.qkv, &e.o, &e.w1}) L->qws = ar.take<int8_t>((size_t)L->N * L->K);
+    if (c.d_ff % 64 == 0)    // the fused FFN's weight stream (F KB per layer)
+      for (auto& e : m->enc) e.ffn = ar.take<int8_t>((size_t)F * 1024);
     for (auto& d : m->dec) {
       lin(d.qkv, 3 * D, D); lin(d.o, D, D); lin(d.cq, D, D); lin(d.ckv, 2 * D, D);
       lin(d.co, D, D); lin(d.w1, F, D); lin(d.w2, D, F);
@@ -421,6 +424,11 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
         qtx_model_destroy(m);
         return fail(QTX_E_HIP, "KP / WS weight pack");
       }
+  for (auto& e : m->enc)
+    if (e.ffn && launch_pack_ffn(e.w1.w8(), e.w2.w8(), F, e.ffn, st) != hipSuccess) {
+      qtx_model_destroy(m);
+      return fail(QTX_E_HIP, "fused FFN weight pack");
+    }
   // norms: order of weights.py:norm_names — enc L x 2, enc final, dec L x 3, dec final
   const int nb = norm_tensor_base(c);
   const int n_norms = 5 * NL + 2;
@@ -909,6 +917,13 @@ int check_fault(const qtx_model* m, const qtx_fault* f, int module, long B, long
   return QTX_OK;
 }
 
+// The fused FFN launch (qtx_ffn.hip) replaces the one-pass FFN1 + the FFN2 row GEMM on the
+// KP path from ffn_fused_min_m rows (QTX_FFN_FUSED_MIN_M; QTX_NO_FFN_FUSED: never): one
+// workgroup per 128 rows, so below ~1 block per CU the split launches use the chip better.
+bool ffn_fused_ok(const EncLayer& L, long M, bool kp) {
+  return kp && L.ffn && !knobs().no_ffn_fused && M >= knobs().ffn_fused_min_m;
+}
+
 int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, int S,
                 float* out, Scratch& s, hipStream_t st, const qtx_fault* f = nullptr,
                 hipEvent_t after_first = nullptr) {
@@ -956,6 +971,22 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
       HIPCHK(ea);
     }
     RC(row_res_ln(L.o, s.a8, s.sa, M, s.x, L.ln[1], s.a8, s.sa, nullptr, st, fa(G_O), kp));
+    if (ffn_fused_ok(L, M, kp)) {
+      // the FFN sublayer in one launch (k_ffn_fused): the hidden stays on chip; each
+      // workgroup reads its rows of a8 / sa before it writes them (the next LN's codes)
+      FfnArgs g{};
+      g.A = s.a8; g.sa = s.sa; g.wf = L.ffn;
+      g.sw1 = L.w1.s; g.b1 = L.w1.b; g.sw2 = L.w2.s; g.b2 = L.w2.b;
+      g.x = s.x; g.M = M; g.F = c.d_ff;
+      if (l + 1 < NL) {
+        g.ln_a = m->enc[l + 1].ln[0][0]; g.ln_b = m->enc[l + 1].ln[0][1];
+        g.lnq = s.a8; g.lns = s.sa;
+      } else {
+        g.ln_a = m->enc_norm[0]; g.ln_b = m->enc_norm[1]; g.lnout = out;
+      }
+      HIPCHK(launch_ffn_fused(g, st));
+      continue;
+    }
     RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1), kp, s.status));
     if (l + 1 < NL)
       RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc[l + 1].ln[0], s.a8, s.sa, nullptr, st,
@@ -1793,6 +1824,28 @@ int32_t qtx_pack_w_kp(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* 
   if (!W || !out) return fail(QTX_E_INVALID, "null argument");
   const hipError_t e = launch_pack_w_kp(W, N, K, out, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "pack_w_kp N=%d K=%d", N, K);
+  HIPCHK(e);
+  return QTX_OK;
+}
+
+int32_t qtx_ffn_rows(const qtx_ffn_args* a, void* stream) {
+  if (!a || !a->A || !a->sa || !a->wf || !a->sw1 || !a->b1 || !a->sw2 || !a->b2 || !a->x ||
+      !a->ln_a || !a->ln_b || (a->lnq ? !a->lns : !a->lnout))
+    return fail(QTX_E_INVALID, "null argument");
+  FfnArgs g{};
+  g.A = a->A; g.sa = a->sa; g.wf = a->wf; g.sw1 = a->sw1; g.b1 = a->b1; g.sw2 = a->sw2;
+  g.b2 = a->b2; g.x = a->x; g.ln_a = a->ln_a; g.ln_b = a->ln_b; g.lnq = a->lnq;
+  g.lns = a->lns; g.lnout = a->lnout; g.M = a->M; g.F = a->F;
+  const hipError_t e = launch_ffn_fused(g, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "ffn_rows: F=%d", a->F);
+  HIPCHK(e);
+  return QTX_OK;
+}
+
+int32_t qtx_pack_ffn(const int8_t* W1, const int8_t* W2, int32_t F, int8_t* out, void* stream) {
+  if (!W1 || !W2 || !out) return fail(QTX_E_INVALID, "null argument");
+  const hipError_t e = launch_pack_ffn(W1, W2, F, out, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "pack_ffn F=%d", F);
   HIPCHK(e);
   return QTX_OK;
 }

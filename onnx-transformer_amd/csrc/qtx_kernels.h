@@ -175,6 +175,26 @@ hipError_t launch_gemm_ws(const RowGemmArgs& a, hipStream_t st);
 hipError_t launch_gemm_wsx(const RowGemmArgs& a, hipStream_t st);
 hipError_t launch_pack_w_ws(const int8_t* W, int N, int K, int8_t* out, hipStream_t st);
 
+// The encoder's FFN sublayer in one launch (qtx_ffn.hip, k_ffn_fused): FFN1 (+ReLU, per-token
+// quantization of the hidden over all F columns) and FFN2 (+residual, next LayerNorm + quant)
+// per 128-row block, the hidden kept on chip.  A: x1q int8 [M (+1 if odd), 512] in the KP
+// layout, sa [M]; wf: the weight stream (launch_pack_ffn); x [M, 512] fp32 residual in,
+// x + FFN(x) out (in place); then LayerNorm(ln_a, ln_b) quantized -> lnq (KP) + lns [M], or
+// fp32 -> lnout when lnq is null.  F % 64 == 0, 256 <= F <= 2048.
+struct FfnArgs {
+  const int8_t* A; const float* sa;
+  const int8_t* wf;
+  const float* sw1; const float* b1;        // [F]
+  const float* sw2; const float* b2;        // [512]
+  float* x;
+  const float* ln_a; const float* ln_b;
+  int8_t* lnq; float* lns; float* lnout;
+  int M, F;
+};
+hipError_t launch_ffn_fused(const FfnArgs& a, hipStream_t st);
+// W1 int8 [F, 512], W2 int8 [512, F] -> the stream k_ffn_fused reads (F * 1024 bytes)
+hipError_t launch_pack_ffn(const int8_t* W1, const int8_t* W2, int F, int8_t* out, hipStream_t st);
+
 hipError_t launch_gemm(const GemmArgs& a, int wbits, hipStream_t st);
 hipError_t launch_skinny(const SkinnyArgs& a, int wbits, hipStream_t st);
 hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st);

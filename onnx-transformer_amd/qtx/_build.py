@@ -14,7 +14,7 @@ CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 REPO = os.path.dirname(os.path.dirname(HERE))
 LIB = os.path.join(HERE, "libqtx.so")
 SOURCES = ["qtx_kernels.hip", "qtx_decode.hip", "qtx_gemm.hip", "qtx_wsgemm.hip", "qtx_attn.hip",
-           "qtx_api.hip", "qtx_knobs.hip"]
+           "qtx_ffn.hip", "qtx_api.hip", "qtx_knobs.hip"]
 # measured-negative kernel variants and their switches: compiled only into the diagnostic
 # library (build(extra=...) -> libqtx_diag.so, with -DQTX_DIAG), never into libqtx.so
 DIAG_SOURCES = ["diag/qtx_wsgemm_diag.hip"]   # csrc/diag/: outside the product sources

@@ -42,6 +42,13 @@ class RowGemm(C.Structure):
                 ("pmax_out", P), ("pmax_in", P), ("pmax_n", I32), ("kp", I32), ("status", P),
                 ("part", P), ("ksplit", I32)]
 
+class FfnRows(C.Structure):
+    """struct qtx_ffn_args (include/qtx.h)."""
+    _fields_ = [("A", P), ("sa", P), ("wf", P), ("sw1", P), ("b1", P), ("sw2", P), ("b2", P),
+                ("x", P), ("ln_a", P), ("ln_b", P), ("lnq", P), ("lns", P), ("lnout", P),
+                ("M", I32), ("F", I32)]
+
+
 class Fault(C.Structure):
     """struct qtx_fault (include/qtx.h)."""
     _fields_ = [("kind", I32), ("module", I32), ("layer", I32), ("linear", I32),
@@ -79,6 +86,8 @@ SIGNATURES = {
     "qtx_linear_rows": (I32, [C.POINTER(RowGemm), P]),
     "qtx_pack_w_kp": (I32, [P, I32, I32, P, P]),
     "qtx_pack_w_ws": (I32, [P, I32, I32, P, P]),
+    "qtx_ffn_rows": (I32, [C.POINTER(FfnRows), P]),
+    "qtx_pack_ffn": (I32, [P, P, I32, P, P]),
     "qtx_pack_int4": (I32, [P, I32, I32, P, P]),
     "qtx_attention_i8": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, P]),
     "qtx_attention_trace": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, P, P, P]),

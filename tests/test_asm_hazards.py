@@ -45,13 +45,13 @@ def test_asm_mfma_wait_states(tmp_path):
 
 @needs_hipcc
 @pytest.mark.parametrize("src", ["qtx_gemm.hip", "qtx_wsgemm.hip", "qtx_attn.hip", "qtx_decode.hip",
-                                 "qtx_kernels.hip"])
+                                 "qtx_kernels.hip", "qtx_ffn.hip"])
 def test_counted_vmcnt_waits_follow_dmas_only(tmp_path, src):
     s = _asm(tmp_path, os.path.join(CSRC, src), src.split(".")[0])
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools/check_vmcnt_order.py"), s],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-3000:]
-    if src == "qtx_gemm.hip":      # the KP row GEMM's counted ring waits are really checked
+    if src in ("qtx_gemm.hip", "qtx_ffn.hip"):   # the rings' counted waits are really checked
         n = int(re.search(r"(\d+) counted vmcnt waits", r.stdout).group(1))
         assert n > 0, r.stdout
 

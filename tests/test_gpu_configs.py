@@ -66,13 +66,14 @@ def cfg3_split(torch, gpu_model, cfg3_inputs):
     return _encode(torch, gpu_model, x, m)
 
 
-def test_cfg3_encoder_two_pass_ffn1_equals_one_pass(torch, gpu_model, cfg3_inputs, cfg3_split,
-                                                   knob_env):
-    """The default encoder (one-pass FFN1 with the in-launch exchange, one stream) against
-    the two-pass FFN1 (QTX_NO_WSX), which also runs the batch as two half-batch streams: the
-    same bits."""
+@pytest.mark.parametrize("env", [{"QTX_FFN_FUSED_MIN_M": 1}, {"QTX_NO_WSX": 1}])
+def test_cfg3_encoder_ffn_paths_agree(torch, gpu_model, cfg3_inputs, cfg3_split, knob_env, env):
+    """The default encoder (the one-pass FFN1 with the in-launch exchange + the FFN2 row
+    GEMM) against the fused FFN launch (k_ffn_fused, QTX_FFN_FUSED_MIN_M) and the two-pass
+    FFN1 (QTX_NO_WSX), which also runs the batch as two half-batch streams — the same bits."""
     x, m = cfg3_inputs
-    knob_env("QTX_NO_WSX", 1)
+    for k, v in env.items():
+        knob_env(k, v)
     np.testing.assert_array_equal(_encode(torch, gpu_model, x, m), cfg3_split)
 
 
@@ -91,19 +92,21 @@ def test_cfg3_encoder_sample_matches_oracle(torch, oracle_model, cfg3_inputs, cf
     np.testing.assert_array_equal(cfg3_split[b:b + 1], oracle_model.encode(x[b:b + 1], m[b:b + 1]))
 
 
-def test_cfg3_encoder_split_two_threads(torch, gpu_model, cfg3_inputs, cfg3_split):
+@pytest.mark.parametrize("env", [{}, {"QTX_FFN_FUSED_MIN_M": 1}])
+def test_cfg3_encoder_split_two_threads(torch, gpu_model, cfg3_inputs, cfg3_split, knob_env, env):
     """Two threads share the model handle, each on its own stream with its own inputs, at
-    the same time: the two streams' one-pass FFN1 launches, whose workgroups wait for their
-    partner slices, run concurrently (work by arrival ticket: no co-residency requirement);
-    with QTX_NO_WSX the two-stream split path's shared second stream and fork / lag / join
-    events are serialized by the model's lock."""
+    the same time, with the one-pass FFN1 whose workgroups wait for their partner slices
+    (work by arrival ticket: no co-residency requirement; the default) and with the fused
+    FFN launch.
+    One round each: the ordering rule these launches depend on (a counted vmcnt never waits
+    past a store, qtx_common.h VM_CNT_ORDER) is checked statically on every CPU run
+    (tests/test_asm_hazards.py), not by repetition here."""
+    for k, v in env.items():
+        knob_env(k, v)
     x, m = cfg3_inputs
     x2 = np.ascontiguousarray(x[::-1])      # a different batch: the sentences reversed
     m2 = np.ascontiguousarray(m[::-1])
-    # several rounds: the race this guards against (a counted vmcnt releasing a block before
-    # its DMA landed, qtx_common.h VM_CNT_ORDER) showed in about one round of six
-    for _ in range(4):
-        _two_threads_round(torch, gpu_model, x, m, x2, m2, cfg3_split)
+    _two_threads_round(torch, gpu_model, x, m, x2, m2, cfg3_split)
 
 
 def _two_threads_round(torch, gpu_model, x, m, x2, m2, cfg3_split):

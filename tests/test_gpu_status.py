@@ -125,6 +125,7 @@ def test_model_reports_device_error(torch, gpu_model, knob_env):
     qtx_model_check (QtxModel.check) raise QTX_E_DEVICE = 5 once; the word is then clear,
     and a clean run stays clean."""
     from qtx._lib import QtxError
+    knob_env("QTX_NO_FFN_FUSED", 1)                    # FFN1 on the one-pass exchange
     x, mk = _cfg3(torch)
     gpu_model.encode(x, mk)
     gpu_model.check()                                  # default bound: clean
@@ -147,6 +148,7 @@ def test_status_word_is_per_call(torch, gpu_model, knob_env):
     stream: B's check is clean and cannot clear A's error; A's check raises."""
     import threading
     from qtx._lib import QtxError
+    knob_env("QTX_NO_FFN_FUSED", 1)                    # FFN1 on the one-pass exchange
     knob_env("QTX_WSX_SPIN_LIMIT", 64)
     knob_env("QTX_WSX_DROP_SLICE", 3)
     xa, ma = _cfg3(torch)

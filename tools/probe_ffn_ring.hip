@@ -41,7 +41,7 @@ __device__ __forceinline__ void dma16(const int8_t* gsrc, const uint8_t* lds_dst
 }
 
 // MODE 0: fill + consume; 1: fill only; 2: consume only (no DMA)
-template <int NW, int NSLOT, bool ROT, bool NT, int MODE, int PD = 0>
+template <int NW, int NSLOT, bool ROT, bool NT, int MODE, int PD = 0, bool SB = false, bool ASM = false, int SYNC = 0>
 __global__ __launch_bounds__(NW * 64) void k_ring(const int8_t* W, int* sink, unsigned long long* out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[NSLOT * SLOT];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(NW * 64) void k_ring(const int8_t* W, int* sink, un
   __syncthreads();
   const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int s = 0; s < NSTREAM; ++s) {
-    if (MODE != 2) {
+    if (MODE != 2 && SYNC != 2) {
       // this wave's pieces of slot s landed: the youngest are slots s+1 .. s+NSLOT-2
       const int ahead = min(NSLOT - 2, NSTREAM - 1 - s);
       if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPW) : "memory");
@@ -87,8 +87,10 @@ __global__ __launch_bounds__(NW * 64) void k_ring(const int8_t* W, int* sink, un
       else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (SYNC != 1) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
     issue(s + NSLOT - 1);
     if (MODE == 1) continue;
     const uint8_t* slot = lds + (s % NSLOT) * SLOT;
@@ -115,13 +117,21 @@ __global__ __launch_bounds__(NW * 64) void k_ring(const int8_t* W, int* sink, un
       for (int f = 0; f < 32; ++f) {
         const v4i cur = b[f % PD];
         if (f + PD < 32) b[f % PD] = *reinterpret_cast<const v4i*>(slot + (f + PD) * 1024 + lane * 16);
+        // pin the prefetch distance: the scheduler would otherwise sink each read next to
+        // its MFMAs (two buffers, the LDS latency exposed every 4 MFMAs)
+        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < RF; ++i)
-          acc[i][f & 7] = __builtin_amdgcn_mfma_i32_16x16x64_i8(cur, xa[i][f & 7], acc[i][f & 7], 0, 0, 0);
+        for (int i = 0; i < RF; ++i) {
+          if constexpr (ASM)   // accumulators pinned to AGPRs, no copies between iterations
+            asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc[i][f & 7]) : "v"(cur), "v"(xa[i][f & 7]));
+          else
+            acc[i][f & 7] = __builtin_amdgcn_mfma_i32_16x16x64_i8(cur, xa[i][f & 7], acc[i][f & 7], 0, 0, 0);
+        }
+        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory");
   int sum = 0;
 #pragma unroll
   for (int i = 0; i < RF; ++i)
@@ -149,19 +159,17 @@ int main() {
     free(h);
   }
   Var vars[] = {
-      {"4w 4slot rotated          ", k_ring<4, 4, true, false, 0>, 256, 0},
-      {"4w consume-only           ", k_ring<4, 4, true, false, 2>, 256, 2},
-      {"4w 4slot rotated pd4      ", k_ring<4, 4, true, false, 0, 4>, 256, 0},
-      {"4w consume-only pd4       ", k_ring<4, 4, true, false, 2, 4>, 256, 2},
-      {"4w 4slot rotated pd8      ", k_ring<4, 4, true, false, 0, 8>, 256, 0},
-      {"4w consume-only pd8       ", k_ring<4, 4, true, false, 2, 8>, 256, 2},
-      {"4w 4slot rotated pd16     ", k_ring<4, 4, true, false, 0, 16>, 256, 0},
-      {"4w consume-only pd16      ", k_ring<4, 4, true, false, 2, 16>, 256, 2},
-      {"4w 5slot rotated pd8      ", k_ring<4, 5, true, false, 0, 8>, 256, 0},
-      {"4w 3slot rotated pd8      ", k_ring<4, 3, true, false, 0, 8>, 256, 0},
-      {"4w 4slot rotated pd8 nt   ", k_ring<4, 4, true, true, 0, 8>, 256, 0},
-      {"8w 4slot rotated pd4      ", k_ring<8, 4, true, false, 0, 4>, 512, 0},
-      {"8w consume-only pd4       ", k_ring<8, 4, true, false, 2, 4>, 512, 2},
+      {"4w consume-only pd4 sb     ", k_ring<4, 4, true, false, 2, 4, true>, 256, 2},
+      {"4w consume-only pd4 asm    ", k_ring<4, 4, true, false, 2, 4, true, true>, 256, 2},
+      {"4w consume-only pd8 asm    ", k_ring<4, 4, true, false, 2, 8, true, true>, 256, 2},
+      {"4w 4slot pd4 asm           ", k_ring<4, 4, true, false, 0, 4, true, true>, 256, 0},
+      {"4w 4slot pd8 asm           ", k_ring<4, 4, true, false, 0, 8, true, true>, 256, 0},
+      {"4w 4slot pd8 asm no-barrier", k_ring<4, 4, true, false, 0, 8, true, true, 1>, 256, 0},
+      {"4w 4slot pd8 asm no-vmwait ", k_ring<4, 4, true, false, 0, 8, true, true, 2>, 256, 0},
+      {"8w consume-only pd4 asm    ", k_ring<8, 4, true, false, 2, 4, true, true>, 512, 2},
+      {"8w 4slot pd4 asm           ", k_ring<8, 4, true, false, 0, 4, true, true>, 512, 0},
+      {"8w 4slot pd4 asm no-barrier", k_ring<8, 4, true, false, 0, 4, true, true, 1>, 512, 0},
+      {"8w 4slot pd4 asm no-vmwait ", k_ring<8, 4, true, false, 0, 4, true, true, 2>, 512, 0},
   };
   printf("CUs %d; per CU %.2f MB streamed (96 x 32 KB slots); MFMA floor at 4 waves = 96 x 64 x 16 cycles\n",
          ncu, 3.0 * NCHUNK * SLOT / 1048576.0);
