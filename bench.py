@@ -13,7 +13,8 @@ the barrier, the max-over-ranks of the elapsed time and, after the timed region,
 all-gather of the ids that rank 0 checks against a re-decoded sample.
 
 Printed JSON (rank 0) adds:
-  roofline     dominant kernel, algorithmic bytes per launch / measured avg duration
+  roofline     decode's dominant kernel, algorithmic bytes per launch / profiled avg duration
+  roofline_encoder  the cfg3 encoder's FFN1 launch against the int8 MFMA peak (+ PMC traffic)
   cpu_baseline oracle/torch_port.py (the reference's fp32 fake-quant arithmetic in torch)
                on bounded samples on the host cores, rank 0 only
   cfg3_encoder encoder-only B=256 S=128 QuantLinear int8 ops/s vs the MFMA int8 peak
@@ -223,6 +224,28 @@ def profiler_dominant(B, alg):
                             "note": "rocprofv3 per-dispatch durations of the graph-replayed "
                                     "decode kernels; the profiler serializes graph dispatches, "
                                     "so they read longer than the live per-node time"}
+    return None
+
+
+# The encoder's north-star kernel (cfg3, BASELINE.json: >= 50 % of the int8-MFMA peak on the
+# encoder QuantLinear GEMMs): the one-pass FFN1 (k_gemm_wsy, M = 32768, N = 2048, K = 512, the
+# ReLU + per-token quantization epilogue), the launch furthest from its roofline.
+ENC_DOMINANT = ("ffn1_quant_onepass", "k_gemm_wsy<0, 1>")
+
+
+def pmc_encoder(kernel):
+    """The newest committed rocprofv3 summary of the cfg3 encoder (tools/pmc_encoder.sh ->
+    profiles/*_pmc_encoder.json) for one kernel: its profiled avg_us, corrected HBM bytes per
+    dispatch (2 x FETCH_SIZE + WRITE_SIZE) and MfmaUtil, with the file it came from."""
+    import glob
+    for fn in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_encoder.json")), reverse=True):
+        with open(fn) as f:
+            d = json.load(f)
+        if kernel in d:
+            k = d[kernel]
+            return {"source": os.path.relpath(fn, REPO), "avg_us": k.get("avg_us"),
+                    "hbm_bytes": k.get("hbm_read_bytes_corrected", 0) + k.get("hbm_write_bytes", 0),
+                    "mfma_util_pct": k.get("MfmaUtil")}
     return None
 
 
@@ -514,19 +537,26 @@ def main():
         # it (its launch boundary included: conservative).  rocprofv3's per-dispatch
         # durations of graph-replayed nodes are inflated by the profiler (an empty kernel
         # reads 4.6 us there, 1.6 us per node live: profiles/r03b_dominant_timing.md)
-        kt = chain_us * 1e-6
         alg = dominant_alg_bytes(Bd)
+        # achieved / frac follow from the committed rocprofv3 summary of this bench (VERDICT
+        # r04: per-dispatch durations, profiles/*_bench_kernel_stats.md); the live chain
+        # timing sits beside it (the profiler serializes graph nodes, so its per-dispatch
+        # times read longer than the live per-node time the decode sees)
+        prof = profiler_dominant(Bd, alg)
+        kt = (prof["avg_us"] if prof else chain_us) * 1e-6
         roof = {"kernel": f"{DOMINANT}: decode O / Oc projection (M={Bd}, N={D}, K={D}, int8, "
                           "fp32 context quantized per token in the prologue, residual epilogue)",
                 "bound": "hbm", "achieved": alg / kt / 1e9, "peak": PEAK_HBM / 1e9,
                 "unit": "GB/s", "frac": alg / kt / PEAK_HBM, "traffic": pmc_traffic(),
-                "avg_us": kt * 1e6, "empty_node_us": nop_us,
-                "marginal_us": chain_us - nop_us, "alg_bytes_per_launch": alg,
-                "profiler": profiler_dominant(Bd, alg),
-                "method": f"hipGraph chain of 256 dependent launches over {DOMINANT_COPIES} "
-                          "rotating operand sets, HIP events on the replay stream: us per node "
-                          "(launch boundary included); empty_node_us = the same chain of empty "
-                          "kernels, marginal_us = the difference"}
+                "avg_us": kt * 1e6, "alg_bytes_per_launch": alg,
+                "source": prof["source"] if prof else "live chain (no committed kernel stats)",
+                "live": {"avg_us": chain_us, "achieved": alg / (chain_us * 1e-6) / 1e9,
+                         "frac": alg / (chain_us * 1e-6) / PEAK_HBM, "empty_node_us": nop_us,
+                         "marginal_us": chain_us - nop_us,
+                         "method": f"hipGraph chain of 256 dependent launches over "
+                                   f"{DOMINANT_COPIES} rotating operand sets, HIP events on the "
+                                   "replay stream: us per node (launch boundary included); "
+                                   "empty_node_us = the same chain of empty kernels"}}
         # the whole decode step: (decode of max_len - 1 steps) - (decode of 1 step), per step
         t_full = time_decode(model, Bd, S, L)
         t_one = time_decode(model, Bd, S, 2)
@@ -587,6 +617,26 @@ def main():
                     "frac": round(r["bound_us"] / g[k][0], 3)} for k, r in rf.items()}
             out["cfg3_encoder"]["frac_of_roofline_quantlinear_gemms"] = bound_us / gemm_us
             out["cfg3_encoder"]["int8_peak_frac_attainable"] = gemm_ops / (bound_us * 1e-6) / PEAK_INT8_OPS
+            # the encoder's north-star kernel against the int8 MFMA peak: live launch time
+            # (HIP events, this run) and the committed profiler view with its PMC HBM traffic
+            name, kname = ENC_DOMINANT
+            us, ops1 = g.get(name, (float("nan"), 0))
+            pe = pmc_encoder(kname)
+            ab = rf[name]["alg_bytes"]
+            out["roofline_encoder"] = {
+                "kernel": f"{kname}: cfg3 FFN1 one pass (M={Bc * Sc}, N={F}, K={D}, int8, ReLU + "
+                          "per-token quantization over all 2048 columns in the epilogue)",
+                "bound": rf[name]["bound"], "achieved": ops1 / (us * 1e-6) / 1e12,
+                "peak": PEAK_INT8_OPS / 1e12, "unit": "TOP/s (int8)",
+                "frac": ops1 / (us * 1e-6) / PEAK_INT8_OPS, "avg_us": us,
+                "alg_bytes_per_launch": ab,
+                "traffic": pe["hbm_bytes"] if pe else None,
+                "traffic_over_alg": (pe["hbm_bytes"] / ab) if pe else None,
+                "profiler": ({"source": pe["source"], "avg_us": pe["avg_us"],
+                              "frac": ops1 / (pe["avg_us"] * 1e-6) / PEAK_INT8_OPS,
+                              "mfma_util_pct": pe["mfma_util_pct"]} if pe else None),
+                "method": "the launch alone at cfg3's M as the encoder runs it (10 launches, HIP "
+                          "events); profiler = the newest profiles/*_pmc_encoder.json"}
             # BASELINE configs 4 and 5 (secondary lines): int4 weights at B=32, and the
             # per-GPU shard of the 8-GPU config (B=2048 / 8 = 256 sentences)
             m4 = QtxModel(sd, ModelConfig(weight_bits=4))

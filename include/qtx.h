@@ -311,10 +311,11 @@ typedef struct qtx_ffn_args {
 } qtx_ffn_args;
 int32_t qtx_ffn_rows(const qtx_ffn_args* args, void* stream);
 /* W1 int8 [F, 512] and W2 int8 [512, F] row-major -> the weight stream qtx_ffn_rows reads
- * (F * 1024 bytes): per 64-column chunk c a 32 KB W1 slot (fragment 4s + j', lane l: W1[64c +
- * 16j' + (l & 15)][64s + 16(l >> 4) .. +16]) and a 32 KB W2 slot (fragment j, lane l: byte
- * 4j' + e = W2[col][64c + 16j' + 4(l >> 4) + e], col = 16(l & 15) + j for j < 16, else
- * 256 + 16(l & 15) + j - 16). */
+ * (F * 1024 bytes): per 64-column chunk c four 16 KB slots of 16 fragments x 64 lanes x 16
+ * bytes — slots 4c + h (h = 0, 1; W1 K steps 4h .. 4h+3), fragment 4s' + j', lane l:
+ * W1[64c + 16j' + (l & 15)][64(4h + s') + 16(l >> 4) .. +16]; slots 4c + 2 + ch (W2, column
+ * half ch), fragment j, lane l: byte 4j' + e = W2[col][64c + 16j' + 4(l >> 4) + e] with
+ * col = 16(l & 15) + 8ch + j for j < 8, else 256 + 16(l & 15) + 8ch + j - 8. */
 int32_t qtx_pack_ffn(const int8_t* W1, const int8_t* W2, int32_t F, int8_t* out, void* stream);
 /* W int8 [N, K] row-major -> out [N, K] in the KP layout with the per-512-column-tile row
  * order qtx_linear_rows(kp = 1) reads.  N % 512 == 0, K % 64 == 0. */

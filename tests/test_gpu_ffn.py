@@ -45,22 +45,25 @@ def from_kp(a, M):
 
 
 def pack_ref(w1, w2):
-    """qtx_pack_ffn's stream (include/qtx.h) restated: [F/64][2][32 fragments][64 lanes][16]."""
+    """qtx_pack_ffn's stream (include/qtx.h) restated: [F/64 chunks][4 slots][16 fragments]
+    [64 lanes][16 bytes]; slots 0, 1 = W1 K steps 0-3 / 4-7, slots 2, 3 = W2 column half 0 / 1."""
     F = w1.shape[0]
     nc = F // 64
-    out = np.zeros((nc, 2, 32, 64, 16), np.int8)
+    out = np.zeros((nc, 4, 16, 64, 16), np.int8)
     lane = np.arange(64)
     f, g = lane & 15, lane >> 4
+    b = np.arange(16)
     for c in range(nc):
-        for fr in range(32):
-            s, j = fr >> 2, fr & 3
-            rows = w1[64 * c + 16 * j + f]                              # [64, 512]
-            idx = 64 * s + 16 * g[:, None] + np.arange(16)[None, :]
-            out[c, 0, fr] = np.take_along_axis(rows, idx, axis=1)
-            col = np.where(fr < 16, 16 * f + fr, 256 + 16 * f + fr - 16)
-            b = np.arange(16)
-            k = 64 * c + 16 * (b[None, :] >> 2) + 4 * g[:, None] + (b[None, :] & 3)
-            out[c, 1, fr] = np.take_along_axis(w2[col], k, axis=1)
+        for fr in range(16):
+            for hh in range(2):
+                s, j = 4 * hh + (fr >> 2), fr & 3
+                rows = w1[64 * c + 16 * j + f]                          # [64, 512]
+                idx = 64 * s + 16 * g[:, None] + b[None, :]
+                out[c, hh, fr] = np.take_along_axis(rows, idx, axis=1)
+            for ch in range(2):
+                col = np.where(fr < 8, 16 * f + 8 * ch + fr, 256 + 16 * f + 8 * ch + fr - 8)
+                k = 64 * c + 16 * (b[None, :] >> 2) + 4 * g[:, None] + (b[None, :] & 3)
+                out[c, 2 + ch, fr] = np.take_along_axis(w2[col], k, axis=1)
     return out.reshape(-1)
 
 

@@ -20,11 +20,33 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int SLOT = 32 * 1024;
 constexpr int NCHUNK = 32;                 // 64-column FFN1 mini-chunks (d_ff 2048)
 constexpr int NSTREAM = 3 * NCHUNK;        // slots consumed per block
+
+// DMA issue forms: 0 global_load_lds 64-bit VGPR address; 1 global_load_lds SGPR base +
+// 32-bit VGPR offset (a buffer_load ... lds with ADD_TID_ENABLE, no VGPR operand at all,
+// faulted on the GPU as first written: not kept)
+template <int DM>
+__device__ __forceinline__ void dmax(const int8_t* base, unsigned off, unsigned voff, const uint8_t* lds_dst) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+  unsigned keep;
+  if constexpr (DM == 0)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(base + off + voff), "s"(dst) : "memory");
+  else if constexpr (DM == 1) {
+    const unsigned long long bb = (unsigned long long)(uintptr_t)base;
+    const unsigned long long sb = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(bb >> 32)) << 32) |
+                                  (unsigned)__builtin_amdgcn_readfirstlane((unsigned)bb);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %3, %1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(sb), "s"(dst), "v"(voff + off) : "memory");
+  }
+}
 
 template <bool NT>
 __device__ __forceinline__ void dma16(const int8_t* gsrc, const uint8_t* lds_dst) {
@@ -41,7 +63,7 @@ __device__ __forceinline__ void dma16(const int8_t* gsrc, const uint8_t* lds_dst
 }
 
 // MODE 0: fill + consume; 1: fill only; 2: consume only (no DMA)
-template <int NW, int NSLOT, bool ROT, bool NT, int MODE, int PD = 0, bool SB = false, bool ASM = false, int SYNC = 0>
+template <int NW, int NSLOT, bool ROT, bool NT, int MODE, int PD = 0, bool SB = false, bool ASM = false, int SYNC = 0, int DM = -1>
 __global__ __launch_bounds__(NW * 64) void k_ring(const int8_t* W, int* sink, unsigned long long* out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[NSLOT * SLOT];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -57,10 +79,16 @@ __global__ __launch_bounds__(NW * 64) void k_ring(const int8_t* W, int* sink, un
   };
   auto issue = [&](int j) {
     if (MODE == 2 || j >= NSTREAM) return;
-    const int8_t* src = W + (long)src_slot(j) * SLOT + (wave * PPW) * 1024 + lane * 16;
     uint8_t* dst = lds + (j % NSLOT) * SLOT + (wave * PPW) * 1024;
+    if constexpr (DM < 0) {
+      const int8_t* src = W + (long)src_slot(j) * SLOT + (wave * PPW) * 1024 + lane * 16;
 #pragma unroll
-    for (int p = 0; p < PPW; ++p) dma16<NT>(src + p * 1024, dst + p * 1024);
+      for (int p = 0; p < PPW; ++p) dma16<NT>(src + p * 1024, dst + p * 1024);
+    } else {
+      const unsigned off = (unsigned)(src_slot(j) * SLOT + (wave * PPW) * 1024);
+#pragma unroll
+      for (int p = 0; p < PPW; ++p) dmax<DM>(W, off + p * 1024, lane * 16, dst + p * 1024);
+    }
   };
   // operands held in registers by the kernel: the block's x1q rows (4 waves: 2 row
   // fragments x 8 K steps; 8 waves: 1 x 8) and FFN2's hq fragments
@@ -159,17 +187,14 @@ int main() {
     free(h);
   }
   Var vars[] = {
-      {"4w consume-only pd4 sb     ", k_ring<4, 4, true, false, 2, 4, true>, 256, 2},
-      {"4w consume-only pd4 asm    ", k_ring<4, 4, true, false, 2, 4, true, true>, 256, 2},
-      {"4w consume-only pd8 asm    ", k_ring<4, 4, true, false, 2, 8, true, true>, 256, 2},
-      {"4w 4slot pd4 asm           ", k_ring<4, 4, true, false, 0, 4, true, true>, 256, 0},
-      {"4w 4slot pd8 asm           ", k_ring<4, 4, true, false, 0, 8, true, true>, 256, 0},
-      {"4w 4slot pd8 asm no-barrier", k_ring<4, 4, true, false, 0, 8, true, true, 1>, 256, 0},
-      {"4w 4slot pd8 asm no-vmwait ", k_ring<4, 4, true, false, 0, 8, true, true, 2>, 256, 0},
-      {"8w consume-only pd4 asm    ", k_ring<8, 4, true, false, 2, 4, true, true>, 512, 2},
-      {"8w 4slot pd4 asm           ", k_ring<8, 4, true, false, 0, 4, true, true>, 512, 0},
-      {"8w 4slot pd4 asm no-barrier", k_ring<8, 4, true, false, 0, 4, true, true, 1>, 512, 0},
-      {"8w 4slot pd4 asm no-vmwait ", k_ring<8, 4, true, false, 0, 4, true, true, 2>, 512, 0},
+      {"8w 4slot pd4 asm  dma global 64b ", k_ring<8, 4, true, false, 0, 4, true, true, 0, 0>, 512, 0},
+      {"8w 4slot pd4 asm  dma global saddr", k_ring<8, 4, true, false, 0, 4, true, true, 0, 1>, 512, 0},
+      {"8w consume-only pd4 asm           ", k_ring<8, 4, true, false, 2, 4, true, true>, 512, 2},
+      {"4w 4slot pd4 asm  dma global 64b  ", k_ring<4, 4, true, false, 0, 4, true, true, 0, 0>, 256, 0},
+      {"4w 4slot pd4 asm  dma global saddr", k_ring<4, 4, true, false, 0, 4, true, true, 0, 1>, 256, 0},
+      {"4w consume-only pd4 asm           ", k_ring<4, 4, true, false, 2, 4, true, true>, 256, 2},
+      {"4w fill-only global 64b           ", k_ring<4, 4, true, false, 1, 0, false, false, 0, 0>, 256, 1},
+      {"4w fill-only global saddr         ", k_ring<4, 4, true, false, 1, 0, false, false, 0, 1>, 256, 1},
   };
   printf("CUs %d; per CU %.2f MB streamed (96 x 32 KB slots); MFMA floor at 4 waves = 96 x 64 x 16 cycles\n",
          ncu, 3.0 * NCHUNK * SLOT / 1048576.0);
