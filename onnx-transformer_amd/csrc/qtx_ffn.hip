@@ -138,8 +138,9 @@ __global__ __launch_bounds__(512) void k_ffn_fused(FfnArgs a) {
     const int r = FULL ? m0 + 32 * rg + 16 * rf + f : min(m0 + 32 * rg + 16 * rf + f, mlast);
     sar[rf] = a.sa[r];
   }
-  // the x1q pieces (the oldest 8 memory operations) landed in every wave, tables written
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  // the x1q pieces landed in every wave (with the first ring slots: a plain vmcnt(0), as
+  // the row scales' loads sit among the youngest operations; VM_CNT_ORDER), tables written
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   QTX_STAMP(1);
 
