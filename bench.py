@@ -307,14 +307,18 @@ def time_row_gemms(M=256 * 128, reps=10, ws=True, operands="encoder"):
         # qtx_api.hip ws_res_ok (the same environment override, the same default)
         o_ws = 2048 <= M < int(os.environ.get("QTX_WS_RES_MAX_M", str(WS_RES_MAX_M)))
         kps[(N, K)] = 2 if (ws and K == D and (N != D or o_ws)) else 1
-        _lib.call("qtx_pack_w_ws" if kps[(N, K)] == 2 else "qtx_pack_w_kp", C.c_void_p(w.data_ptr()),
-                  N, K, C.c_void_p(wk.data_ptr()), C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if kps[(N, K)] == 2 and N in (3 * D, F) and os.environ.get("QTX_WS32", "0") == "1":
+            kps[(N, K)] = 4                  # W in the WS32 layout, as the encoder with QTX_WS32
+        _lib.call({1: "qtx_pack_w_kp", 2: "qtx_pack_w_ws", 4: "qtx_pack_w_ws32"}[kps[(N, K)]],
+                  C.c_void_p(w.data_ptr()), N, K, C.c_void_p(wk.data_ptr()),
+                  C.c_void_p(torch.cuda.current_stream().cuda_stream))
         W[(N, K)] = wk
     cases = [("qkv_quant", 3 * D, D, a512, dict(epi=0, out8=out8, ldo8=D, o8_ts=M * D, os=os_, os_ts=M)),
              ("o_res_ln", D, D, a512, dict(epi=1, res=x, xout=x, ln_a=lna, ln_b=lnb, lnq=out8, lns=os_)),
              # FFN1 in one pass (kp = 3: the slices' row maxima exchanged in-launch; pmax_out
              # is the exchange scratch), as the encoder runs it
-             ("ffn1_quant_onepass", F, D, a512, dict(epi=3, kp=3, pmax_out=gx, out8=out8, ldo8=F, os=os_)),
+             ("ffn1_quant_onepass", F, D, a512, dict(epi=3, kp=5 if kps[(F, D)] == 4 else 3, pmax_out=gx,
+                                                     out8=out8, ldo8=F, os=os_)),
              ("ffn2_res_ln", D, F, a2048, dict(epi=1, res=x, xout=x, ln_a=lna, ln_b=lnb, lnq=out8, lns=os_))]
     if os.environ.get("QTX_BENCH_FFN1_2PASS", "0") == "1":
         # FFN1 as two weight-stationary passes (row maxima, then ReLU + quant from them)

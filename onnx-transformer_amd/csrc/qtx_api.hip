@@ -66,6 +66,7 @@ struct QLin {
   int N = 0, K = 0;
   int8_t* qkp = nullptr;   // encoder, 8-bit: q in the row GEMM's KP layout (pack_w_kp)
   int8_t* qws = nullptr;   // encoder, 8-bit, K == 512: q in the weight-stationary order
+  int8_t* qws32 = nullptr; // encoder Q/K/V, FFN1: q in the WS32 order (k_gemm_wsq32 / wsy32)
   // 4-bit models: the int4 values (in [-7, 7]) unpacked to int8 [N, K] once at load, so the
   // int8 kernels run them — exact (integer products), and the decode is latency-bound, so
   // the packed form's half bytes bought nothing while its unpack lengthened every kernel
@@ -341,8 +342,10 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     for (auto& e : m->enc)
         for (QLin* L : {&e.qkv, &e.o, &e.w1, &e.w2}) L->qkp = ar.take<int8_t>((size_t)L->N * L->K);
     if (c.d_ff % 512 == 0)   // weight-stationary copies (K = 512 GEMMs)
-      for (auto& e : m->enc)
+      for (auto& e : m->enc) {
         for (QLin* L : {&e.qkv, &e.o, &e.w1}) L->qws = ar.take<int8_t>((size_t)L->N * L->K);
+        for (QLin* L : {&e.qkv, &e.w1}) L->qws32 = ar.take<int8_t>((size_t)L->N * L->K);
+      }
     if (c.d_ff % 64 == 0)    // the fused FFN's weight stream (F KB per layer)
       for (auto& e : m->enc) e.ffn = ar.take<int8_t>((size_t)F * 1024);
     for (auto& d : m->dec) {
@@ -420,7 +423,8 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
   for (auto& e : m->enc)
     for (QLin* L : {&e.qkv, &e.o, &e.w1, &e.w2})
       if ((L->qkp && launch_pack_w_kp(L->w8(), L->N, L->K, L->qkp, st) != hipSuccess) ||
-          (L->qws && launch_pack_w_ws(L->w8(), L->N, L->K, L->qws, st) != hipSuccess)) {
+          (L->qws && launch_pack_w_ws(L->w8(), L->N, L->K, L->qws, st) != hipSuccess) ||
+          (L->qws32 && launch_pack_w_ws32(L->w8(), L->N, L->K, L->qws32, st) != hipSuccess)) {
         qtx_model_destroy(m);
         return fail(QTX_E_HIP, "KP / WS weight pack");
       }
@@ -662,13 +666,16 @@ RowGemmArgs rowgemm(const QLin& L, const int8_t* a8, const float* sa, int M, int
   RowGemmArgs g{};
   const bool ws = kp && L.qws && L.K == 512 &&
                   (epi == RE_RES_LN ? ws_res_ok(M) : M >= ws_min_m());
-  g.A = a8; g.lda = L.K; g.sa = sa; g.W = ws ? L.qws : kp ? L.qkp : L.w8(); g.ldw = L.K;
+  // Q/K/V on the 32x32x32 MFMA kernel (QTX_WS32)
+  const bool ws32 = ws && epi == RE_QUANT && L.qws32 && knobs().ws32;
+  g.A = a8; g.lda = L.K; g.sa = sa; g.W = ws32 ? L.qws32 : ws ? L.qws : kp ? L.qkp : L.w8();
+  g.ldw = L.K;
   g.sw = L.s; g.bias = L.b;
-  g.M = M; g.N = L.N; g.K = L.K; g.epi = epi; g.kp = ws ? 2 : kp;
+  g.M = M; g.N = L.N; g.K = L.K; g.epi = epi; g.kp = ws32 ? 4 : ws ? 2 : kp;
   return g;
 }
 hipError_t launch_row_gemm_any(const RowGemmArgs& g, hipStream_t st) {
-  return g.kp == 2 ? launch_gemm_ws(g, st) : launch_gemm_row(g, st);
+  return g.kp == 2 || g.kp == 4 ? launch_gemm_ws(g, st) : launch_gemm_row(g, st);
 }
 // out = per-token quantized (a8 . W^T) per 512-wide tile into out8 + t*M*512, os + t*M
 int row_quant(const QLin& L, const int8_t* a8, const float* sa, int M, int8_t* out8,
@@ -709,6 +716,7 @@ int row_ffn1(const qtx_config& c, const QLin& L, const int8_t* a8, const float* 
   RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RELU_PMAX, kp);
   if (g.kp == 2 && L.N == 2048 && fa.kind == FK_NONE && wsx_on()) {
     g.epi = RE_RELU_QUANT_PMAX;
+    if (L.qws32 && knobs().ws32) { g.W = L.qws32; g.kp = 5; }   // k_gemm_wsy32
     g.pmax_out = s.y;                // granules + ticket: <= 32 * M + 2048 bytes of the (unused) fp32 GEMM scratch
     g.out8 = s.h8; g.ldo8 = c.d_ff; g.os = s.sh;
     g.status = status;               // the model's status word: a timeout becomes an error
@@ -1809,10 +1817,10 @@ int32_t qtx_linear_rows(const qtx_row_gemm* a, void* stream) {
                    (g.lnq ? g.lns != nullptr : g.lnout != nullptr)) ||
                   (g.epi == RE_RELU_PMAX && g.pmax_out) ||
                   (g.epi == RE_RELU_QUANT_PMAX && g.out8 && g.os &&
-                   (g.kp == 3 ? g.pmax_out != nullptr : (g.pmax_in && g.pmax_n > 0)));
+                   (g.kp == 3 || g.kp == 5 ? g.pmax_out != nullptr : (g.pmax_in && g.pmax_n > 0)));
   if (!ok) return fail(QTX_E_INVALID, "operands missing for epi %d", g.epi);
-  const hipError_t e = g.kp == 3   ? launch_gemm_wsx(g, (hipStream_t)stream)
-                       : g.kp == 2 ? launch_gemm_ws(g, (hipStream_t)stream)
+  const hipError_t e = g.kp == 3 || g.kp == 5 ? launch_gemm_wsx(g, (hipStream_t)stream)
+                       : g.kp == 2 || g.kp == 4 ? launch_gemm_ws(g, (hipStream_t)stream)
                                    : launch_gemm_row(g, (hipStream_t)stream);
   if (e == hipErrorInvalidValue)
     return fail(QTX_E_UNSUPPORTED, "rows GEMM: N=%d K=%d epi=%d kp=%d", g.N, g.K, g.epi, g.kp);
@@ -1854,6 +1862,14 @@ int32_t qtx_pack_w_ws(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* 
   if (!W || !out) return fail(QTX_E_INVALID, "null argument");
   const hipError_t e = launch_pack_w_ws(W, N, K, out, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "pack_w_ws N=%d K=%d", N, K);
+  HIPCHK(e);
+  return QTX_OK;
+}
+
+int32_t qtx_pack_w_ws32(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* stream) {
+  if (!W || !out) return fail(QTX_E_INVALID, "null argument");
+  const hipError_t e = launch_pack_w_ws32(W, N, K, out, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "pack_w_ws32 N=%d K=%d", N, K);
   HIPCHK(e);
   return QTX_OK;
 }

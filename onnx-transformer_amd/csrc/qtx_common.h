@@ -14,6 +14,7 @@
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef float v4f __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
 
 // In-kernel phase stamps for diagnosis (tools/kernel_bench.py --stamps): compiled in only
 // with -DQTX_STAMPS; thread 0 of each block records s_memtime at phase boundaries into

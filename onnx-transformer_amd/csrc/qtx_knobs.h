@@ -33,6 +33,7 @@ struct Knobs {
   long ws_min_m = 2048;      // QTX_WS_MIN_M: weight-stationary from this many rows
   long ws_res_min_m = 2048;  // QTX_WS_RES_MIN_M / _MAX_M: the O-projection's WS range
   long ws_res_max_m = 8192;
+  bool ws32 = false;         // QTX_WS32: Q/K/V on k_gemm_wsq32 (v_mfma_i32_32x32x32_i8)
   bool no_ffn_fused = false; // QTX_NO_FFN_FUSED: the encoder FFN as FFN1 + FFN2 launches
   // QTX_FFN_FUSED_MIN_M: the fused FFN launch from this many rows (default: off — measured
   // slower than the split launches at cfg3, DESIGN.md §4 "The fused FFN kernel")

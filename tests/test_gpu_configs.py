@@ -66,11 +66,13 @@ def cfg3_split(torch, gpu_model, cfg3_inputs):
     return _encode(torch, gpu_model, x, m)
 
 
-@pytest.mark.parametrize("env", [{"QTX_FFN_FUSED_MIN_M": 1}, {"QTX_NO_WSX": 1}])
+@pytest.mark.parametrize("env", [{"QTX_FFN_FUSED_MIN_M": 1}, {"QTX_NO_WSX": 1}, {"QTX_WS32": 1},
+                                 {"QTX_WS32": 0}])
 def test_cfg3_encoder_ffn_paths_agree(torch, gpu_model, cfg3_inputs, cfg3_split, knob_env, env):
     """The default encoder (the one-pass FFN1 with the in-launch exchange + the FFN2 row
-    GEMM) against the fused FFN launch (k_ffn_fused, QTX_FFN_FUSED_MIN_M) and the two-pass
-    FFN1 (QTX_NO_WSX), which also runs the batch as two half-batch streams — the same bits."""
+    GEMM) against the fused FFN launch (k_ffn_fused, QTX_FFN_FUSED_MIN_M), the two-pass
+    FFN1 (QTX_NO_WSX), which also runs the batch as two half-batch streams, and Q/K/V on
+    either weight-stationary kernel (k_gemm_wsq32 / k_gemm_wsq, QTX_WS32) — the same bits."""
     x, m = cfg3_inputs
     for k, v in env.items():
         knob_env(k, v)

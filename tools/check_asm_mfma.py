@@ -9,7 +9,8 @@ conservatively (a label resets nothing: the check is linear over the text).
 import re
 import sys
 
-PAD = 18
+PAD = 18          # 16x16x64 (8 passes); the 16-pass 32x32x32 results: PAD32
+PAD32 = 20
 REG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
 
 
@@ -49,12 +50,12 @@ def check(lines, name):
                         print(f"{name}:{ln}: VALU write {sorted(r & srcs)} {age} wait states before asm MFMA")
                         bad += 1
                 pending = [p for p in pending if not (p[0] & dst)]
-                pending.append([dst, PAD])
+                pending.append([dst, PAD32 if "32x32" in op else PAD])
         else:
             used = regs(ops)
             for dst, left in pending:
                 if dst & used and not op.startswith("s_"):
-                    print(f"{name}:{ln}: {op} touches {sorted(dst & used)[:4]} {PAD - left} wait states after asm MFMA")
+                    print(f"{name}:{ln}: {op} touches {sorted(dst & used)[:4]} ({left} wait states short) after asm MFMA")
                     bad += 1
             if op.startswith("v_") and not op.startswith("v_mfma"):
                 w = regs(ops.split(",")[0])
