@@ -307,9 +307,9 @@ def time_row_gemms(M=256 * 128, reps=10, ws=True, operands="encoder"):
         # qtx_api.hip ws_res_ok (the same environment override, the same default)
         o_ws = 2048 <= M < int(os.environ.get("QTX_WS_RES_MAX_M", str(WS_RES_MAX_M)))
         kps[(N, K)] = 2 if (ws and K == D and (N != D or o_ws)) else 1
-        if kps[(N, K)] == 2 and N in (3 * D, F) and os.environ.get("QTX_WS32", "0") == "1":
-            kps[(N, K)] = 4                  # W in the WS32 layout, as the encoder with QTX_WS32
-        _lib.call({1: "qtx_pack_w_kp", 2: "qtx_pack_w_ws", 4: "qtx_pack_w_ws32"}[kps[(N, K)]],
+        if kps[(N, K)] == 2 and N in (3 * D, F) and os.environ.get("QTX_WS32", "0") != "0":
+            kps[(N, K)] = 4                  # W in the WS32 layout (diagnostic library, QTX_WS32)
+        _lib.call({1: "qtx_pack_w_kp", 2: "qtx_pack_w_ws", 4: "qtx_debug_pack_w_ws32"}[kps[(N, K)]],
                   C.c_void_p(w.data_ptr()), N, K, C.c_void_p(wk.data_ptr()),
                   C.c_void_p(torch.cuda.current_stream().cuda_stream))
         W[(N, K)] = wk

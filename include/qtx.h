@@ -278,9 +278,8 @@ typedef struct qtx_row_gemm {
    * maximum is exchanged between the column slices' workgroups inside the launch, so
    * pmax_in / pmax_n are not read; pmax_out is the exchange scratch (>= 32 * M + 2048 bytes,
    * overwritten).  The encoder's FFN1 (qtx_encoder_forward at M >= 2048).
-   * kp = 4: epi 0 (per-token quant) on the 32x32x32-MFMA weight-stationary kernel, W packed
-   * by qtx_pack_w_ws32; outputs exactly as kp = 2 (the encoder's Q/K/V with QTX_WS32).
-   * kp = 5: kp = 3 with W packed by qtx_pack_w_ws32 (the encoder's FFN1 with QTX_WS32). */
+   * kp = 4 / 5 (diagnostic library only: QTX_UNSUPPORTED here): kp = 2 epi 0 / kp = 3 on the
+   * 32x32x32-MFMA kernels, W in their WS32 layout. */
   int32_t kp;
   /* kp = 3 only: device word OR-ed with 1 when a wait for the partner slices' row maxima
    * timed out (the affected codes came from a partial maximum: the call's outputs are
@@ -329,12 +328,6 @@ int32_t qtx_pack_w_kp(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* 
  * W[512t + 64w + 16((l & 15) >> 2) + 4j + (l & 3)][64s + 16(l >> 4) .. +16].
  * N % 512 == 0, K == 512. */
 int32_t qtx_pack_w_ws(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* stream);
-/* W int8 [N, 512] row-major -> out (N*512 bytes) in the order qtx_linear_rows(kp = 4, 5) reads:
- * for 512-column slice t, wave w (0..7), K step s (0..15, 32 bytes), column tile u (0..1) one
- * 1 KB block at ((t*8 + w)*16 + s)*2 + u whose 16-byte lane l (0..63) holds
- * W[512t + 64w + 32u + 16((r >> 2) & 1) + 4(r >> 3) + (r & 3)][32s + 16(l >> 5) .. +16], r = l & 31.
- * N % 512 == 0, K == 512. */
-int32_t qtx_pack_w_ws32(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* stream);
 
 /* Skinny int8 GEMM for decode (M small): out = epilogue(A . W^T) with the A operand made
  * in the prologue: amode 0 = int8 A [M,K] + sa; 1 = LayerNorm(X [M,512]; ln_a, ln_b) then

@@ -1393,6 +1393,525 @@ __global__ __launch_bounds__(512) void k_gemm_wsx(RowGemmArgs g) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// The same statements for v_mfma_i32_32x32x32_i8 (k_gemm_wsq32, this file): 16 accumulators per lane,
+// 16 passes, so the settle pad is 24 wait states.
+template <bool Z, typename T>
+__device__ __forceinline__ void mfma32_pin(v16i& acc, const v4i& w, const v4i& a, float before, T& after) {
+  if constexpr (Z)
+    asm volatile("v_mfma_i32_32x32x32_i8 %0, %2, %3, 0" : "=&v"(acc), "+v"(after) : "v"(w), "v"(a), "v"(before));
+  else
+    asm volatile("v_mfma_i32_32x32x32_i8 %0, %2, %3, %0" : "+v"(acc), "+v"(after) : "v"(w), "v"(a), "v"(before));
+}
+template <bool Z>
+__device__ __forceinline__ void mfma32_asm(v16i& acc, const v4i& w, const v4i& a) {
+  if constexpr (Z)
+    asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, 0" : "=&v"(acc) : "v"(w), "v"(a));
+  else
+    asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+v"(acc) : "v"(w), "v"(a));
+}
+__device__ __forceinline__ void mfma32_settle(v16i (&acc)[2]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc[0]), "+v"(acc[1]));
+}
+
+// =====================================================================================
+// k_gemm_wsq32: k_gemm_wsq on v_mfma_i32_32x32x32_i8.  The round-4 fill probe
+// (profiles/r04_mfma_fill_probe.log) measured ~4 VALU per 32x32x32 MFMA riding free beside
+// two waves per SIMD and ~3.5 cycles per further one (16x16x64: ~2 free, ~4.3 each), so the
+// same epilogue per MAC prices ~15 % lower; one output per MFMA is pinned between them.
+// Tile: C^T = W . A^T per wave: 2 feature tiles of 32 (u) x 32 tokens, 16 K steps of 32 B.
+// The W rows are permuted at pack time (k_pack_w_ws32) so that lane l's 16 accumulators of
+// tile u are 16 CONSECUTIVE output columns 64w + 32u + 16 (l >> 5) .. + 15 of token
+// l & 31: one 16-byte store per tile, one row scale per lane (no broadcast), and a token's
+// partial max over the wave's 64 columns in one cross-lane step (lanes l, l ^ 32).
+// Layouts (K = 512):
+//   W  "WS32": slice t, wave w, K step s (32 B), tile u: 1 KB in MFMA operand order, lane l
+//      = W[n][32s + 16(l >> 5) .. + 16] with n = 512t + 64w + 32u + phi(l & 31),
+//      phi(r) = 16 ((r >> 2) & 1) + 4 (r >> 3) + (r & 3)  (D row r of the 32x32 result).
+//   LDS A piece s (1 KB): lane l = token l & 31, bytes 32s + 16 (l >> 5) .. + 16.
+// Numerics, barriers, DMA and store counts: k_gemm_wsq's.
+// Measured (round 5, tools/ws32_ab.py, three alternated rounds in one process): Q/K/V
+// 39.7 us against k_gemm_wsq's 39.4, with all of W in registers (SR = 16) 38.4; the
+// one-pass FFN1 on k_gemm_wsy32 64.5-72.9 against 58.7-69.2 us; the cfg3 encoder the same
+// within noise (1.661-1.681 vs 1.660-1.672 ms).  Diagnostic build only.
+// =====================================================================================
+constexpr int W32_SR = 10;                       // K steps (of 16) of W in registers
+template <int XG = 1, int SR = W32_SR>   // SR: K steps of W in registers (16: all of W)
+__global__ __launch_bounds__(512) void k_gemm_wsq32(RowGemmArgs g) {
+  constexpr int WL = 8 * (16 - SR) * 2 * 1024 + 16;  // W's LDS part: 96 KB at SR = 10
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4 + 2 * 8 * 64 * 4];
+  uint8_t* const wl = lds + 2 * WP_STAGE;
+  float* const swl = reinterpret_cast<float*>(wl + WL);
+  float* const red0 = swl + 1024;                            // [2][8][32]
+  float* const sal = red0 + 2 * 8 * WP_R;                    // [2][8 waves][64]: row scales
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tok = lane & 31, hh = lane >> 5;
+  const int nsl = g.N >> 9;
+  const int wpt = gridDim.x / nsl;
+  int t = blockIdx.x % nsl, r0 = blockIdx.x / nsl;
+  if (XG) {
+    const int b = blockIdx.x, A = gridDim.x / (8 * nsl), aligned = 8 * nsl * A;
+    if (b < aligned) {
+      const int j = b >> 3;
+      t = j % nsl;
+      r0 = 8 * (j / nsl) + (b & 7);
+    } else {
+      t = (b - aligned) % nsl;
+      r0 = 8 * A + (b - aligned) / nsl;
+    }
+  }
+  const int nb = (g.M + WP_R - 1) / WP_R;
+  if (r0 >= nb) return;
+  const int nblk = (nb - r0 + wpt - 1) / wpt;
+
+  auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto dma4 = [](const float* gsrc, const float* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto rbk = [&](int k) { return r0 + min(k, nblk - 1) * wpt; };
+  // block k: wave w brings A pieces 2w, 2w + 1 and (as k_gemm_wsq) its copy of the 32 row scales
+  auto issue = [&](int k) {
+    uint8_t* st = lds + (k & 1) * WP_STAGE;
+    const long row = min(rbk(k) * WP_R + tok, g.M - 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int s = 2 * wave + i;
+      dma16(g.A + kp_off(row, 32 * s + 16 * hh, WS_K), st + (s << 10));
+    }
+    dma4(g.sa + min(rbk(k) * WP_R + tok, g.M - 1), sal + ((k & 1) * 8 + wave) * 64);
+  };
+  issue(0);
+  v4i wr[SR][2];
+  {
+    const int8_t* wsrc = g.W + ((long)(t * 8 + wave) << 15);
+    const v4i* ws = reinterpret_cast<const v4i*>(wsrc) + lane;
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) wr[s][u] = ws[(s * 2 + u) * 64];
+#pragma unroll
+    for (int p = 0; p < (16 - SR) * 2; ++p)
+      dma16(wsrc + ((SR * 2 + p) << 10) + lane * 16, wl + ((wave * (16 - SR) * 2 + p) << 10));
+    if (wave < 4) {
+      const int c = 128 * wave + 2 * lane;
+      *reinterpret_cast<float2*>(swl + c) = *reinterpret_cast<const float2*>(g.sw + 512 * t + c);
+      *reinterpret_cast<float2*>(swl + 512 + c) = *reinterpret_cast<const float2*>(g.bias + 512 * t + c);
+    }
+#pragma unroll
+    for (int s = 0; s < SR; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) asm volatile("" ::"v"(wr[s][u]));
+  }
+  const __amdgpu_buffer_rsrc_t orsrc = ws_rsrc(g.out8 + (long)t * g.o8_ts, (long)g.M * g.ldo8);
+  const __amdgpu_buffer_rsrc_t srsrc = ws_rsrc(g.os + (long)t * g.os_ts, 4L * g.M);
+  auto redb = [&](int k) { return red0 + (k & 1) * 8 * WP_R; };
+  auto top_wait = [&]() {
+    __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
+    __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+    __builtin_amdgcn_s_barrier();
+  };
+  // y of block k and the wave's partial row maxima into red[k & 1]; lane: token tok,
+  // columns 64 wave + 32 u + 16 hh + r
+  auto form_y = [&](v16i (&acc)[2], float (&y)[2][16], int k) {
+    const float sr = sal[((k & 1) * 8 + wave) * 64 + lane];
+    float am = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 64 * wave + 32 * u + 16 * hh + 4 * q;
+        const float4 s4 = *reinterpret_cast<const float4*>(swl + c);
+        const float4 b4 = *reinterpret_cast<const float4*>(swl + 512 + c);
+        const float swq[4] = {s4.x, s4.y, s4.z, s4.w}, bq4[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          y[u][4 * q + e] = ((float)acc[u][4 * q + e] * sr) * swq[e] + bq4[e];
+          am = fmaxf(am, fabsf(y[u][4 * q + e]));
+        }
+      }
+    am = fmaxf(am, __shfl_xor(am, 32));
+    if (lane < 32) redb(k)[wave * WP_R + lane] = am;
+  };
+  // the scale of block k's rows: lane's token only (no broadcast needed)
+  auto scales = [&](int k, float& bq, float& iq) {
+    const float* red = redb(k);
+    float m = red[tok];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w * WP_R + tok]);
+    bq = scale127(fmaxf(m, 1e-5f));
+    iq = rcp_cr(bq);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bq), srsrc, 4 * (rbk(k) * WP_R + tok), 0, 0);
+  };
+  auto store_tile = [&](int k, int u, const uint32_t (&d)[4]) {
+    const long row = rbk(k) * WP_R + tok;
+    __builtin_amdgcn_raw_buffer_store_b128(v4u{d[0], d[1], d[2], d[3]}, orsrc,
+                                           (int)(row * g.ldo8 + 64 * wave + 32 * u + 16 * hh), 0, 0);
+  };
+  // the 32 MFMAs of block k into acc; with q: block k-1's 32 quantized outputs, one pinned
+  // after each MFMA
+  auto mfma_block = [&](v16i (&acc)[2], const uint8_t* cur, bool q, int kq, float (&y)[2][16]) {
+    float bq = 0.0f, iq = 0.0f;
+    if (q) scales(kq, bq, iq);
+    float hist = 0.0f, tq[4];
+    uint32_t d[4];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const v4i x = *reinterpret_cast<const v4i*>(cur + (s << 10) + lane * 16);
+      v4i w[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        w[u] = s < SR ? wr[s < SR ? s : 0][u]
+                          : *reinterpret_cast<const v4i*>(wl + (((wave * (16 - SR) + s - SR) * 2 + u) << 10) + lane * 16);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (!q) {
+          if (s == 0) mfma32_asm<true>(acc[u], w[u], x);
+          else mfma32_asm<false>(acc[u], w[u], x);
+        } else {
+          const int o = 2 * s + u, uo = o >> 4, r = o & 15;
+          float yv = y[uo][r];
+          if (s == 0) mfma32_pin<true>(acc[u], w[u], x, hist, yv);
+          else mfma32_pin<false>(acc[u], w[u], x, hist, yv);
+          tq[r & 3] = rint_biased(div_cr(yv, bq, iq));
+          hist = tq[r & 3];
+          if ((r & 3) == 3) {
+            d[r >> 2] = pack4_biased(tq[0], tq[1], tq[2], tq[3]);
+            if (r == 15) store_tile(kq, uo, d);
+          }
+        }
+      }
+    }
+    mfma32_settle(acc);
+    if (!q) {           // the 3 stores per iteration of the q path (dropped)
+      const __amdgpu_buffer_rsrc_t nul = ws_rsrc(g.out8, 0L);
+#pragma unroll
+      for (int d2 = 0; d2 < 3; ++d2) __builtin_amdgcn_raw_buffer_store_b32(0u, nul, 0, 0, 0);
+    }
+  };
+
+  v16i acc[2];
+  float y[2][16];
+  __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
+  __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+  __builtin_amdgcn_s_barrier();
+  issue(1);
+  mfma_block(acc, lds, false, 0, y);
+  form_y(acc, y, 0);
+  for (int k = 1; k < nblk; ++k) {
+    top_wait();
+    issue(k + 1);
+    mfma_block(acc, lds + (k & 1) * WP_STAGE, true, k - 1, y);
+    form_y(acc, y, k);
+  }
+  top_wait();
+  {
+    float bq, iq;
+    scales(nblk - 1, bq, iq);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      uint32_t d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        d[j] = pack4_biased(rint_biased(div_cr(y[u][4 * j], bq, iq)),
+                            rint_biased(div_cr(y[u][4 * j + 1], bq, iq)),
+                            rint_biased(div_cr(y[u][4 * j + 2], bq, iq)),
+                            rint_biased(div_cr(y[u][4 * j + 3], bq, iq)));
+      store_tile(nblk - 1, u, d);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// =====================================================================================
+// k_gemm_wsy32: k_gemm_wsy on v_mfma_i32_32x32x32_i8 (W in the WS32 layout, k_gemm_wsq32's
+// tile: lane l = token l & 31 x 16 consecutive columns 64w + 32u + 16 (l >> 5) per tile u).
+// Tickets, granules, the bounded partner waits, wave 0's gather and the two-parity y
+// buffers are k_gemm_wsy's; the hidden is written KP as there.
+// =====================================================================================
+__global__ __launch_bounds__(512) void k_gemm_wsy32(RowGemmArgs g) {
+  constexpr int WL = 8 * (16 - W32_SR) * 2 * 1024;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WP_STAGE + WL + 4096 + 2 * 8 * WP_R * 4 + 2 * 8 * 64 * 4 +
+                                                      2 * 2 * WP_R * 4];
+  uint8_t* const wl = lds + 2 * WP_STAGE;
+  float* const swl = reinterpret_cast<float*>(wl + WL);
+  float* const red0 = swl + 1024;                            // [2][8][32]
+  float* const sal = red0 + 2 * 8 * WP_R;                    // [2][8 waves][64]: row scales
+  float* const gsc = sal + 2 * 8 * 64;                       // [2][2][32]: s and RN(1/s)
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tok = lane & 31, hh = lane >> 5;
+  const int nb = (g.M + WP_R - 1) / WP_R;
+  unsigned long long* const gran = reinterpret_cast<unsigned long long*>(g.pmax_out);
+  __shared__ int ticket;
+  if (tid == 0)
+    ticket = (int)atomicAdd(reinterpret_cast<unsigned*>(gran + 4L * 32 * nb), 1u);
+  __syncthreads();
+  const int q = ticket, wpt = gridDim.x >> 2;       // tickets as in k_gemm_wsx
+  const int t = (q >> 3) & 3, r0 = (q & 7) + 8 * (q >> 5);
+  if (r0 >= nb) return;
+  const int nblk = (nb - r0 + wpt - 1) / wpt;
+
+  auto dma16 = [](const int8_t* gsrc, const uint8_t* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto rbk = [&](int k) { return r0 + min(k, nblk - 1) * wpt; };
+  auto dma4 = [](const float* gsrc, const float* lds_dst) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto issue = [&](int k) {      // block k's A pieces 2w, 2w + 1 and its row scales
+    uint8_t* st = lds + (k & 1) * WP_STAGE;
+    const long row = min(rbk(k) * WP_R + tok, g.M - 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int s = 2 * wave + i;
+      dma16(g.A + kp_off(row, 32 * s + 16 * hh, WS_K), st + (s << 10));
+    }
+    dma4(g.sa + min(rbk(k) * WP_R + tok, g.M - 1), sal + ((k & 1) * 8 + wave) * 64);
+  };
+  issue(0);
+  v4i wr[W32_SR][2];
+  {
+    const int8_t* wsrc = g.W + ((long)(t * 8 + wave) << 15);
+    const v4i* ws = reinterpret_cast<const v4i*>(wsrc) + lane;
+#pragma unroll
+    for (int s = 0; s < W32_SR; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) wr[s][u] = ws[(s * 2 + u) * 64];
+#pragma unroll
+    for (int p = 0; p < (16 - W32_SR) * 2; ++p)
+      dma16(wsrc + ((W32_SR * 2 + p) << 10) + lane * 16, wl + ((wave * (16 - W32_SR) * 2 + p) << 10));
+    if (wave < 4) {
+      const int c = 128 * wave + 2 * lane;
+      *reinterpret_cast<float2*>(swl + c) = *reinterpret_cast<const float2*>(g.sw + 512 * t + c);
+      *reinterpret_cast<float2*>(swl + 512 + c) = *reinterpret_cast<const float2*>(g.bias + 512 * t + c);
+    }
+#pragma unroll
+    for (int s = 0; s < W32_SR; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) asm volatile("" ::"v"(wr[s][u]));
+  }
+  const int c0 = 512 * t + 64 * wave + 16 * hh;   // + 32 u: the lane's first column of tile u
+  const __amdgpu_buffer_rsrc_t orsrc = ws_rsrc(g.out8, (long)(g.M + (g.M & 1)) * g.ldo8);
+  const __amdgpu_buffer_rsrc_t srsrc = ws_rsrc(g.os, t == 0 ? 4L * g.M : 0L);
+  auto redb = [&](int k) { return red0 + (k & 1) * 8 * WP_R; };
+  auto dummy_stores = [&]() {
+    const __amdgpu_buffer_rsrc_t nul = ws_rsrc(g.out8, 0L);
+#pragma unroll
+    for (int d2 = 0; d2 < 3; ++d2) __builtin_amdgcn_raw_buffer_store_b32(0u, nul, 0, 0, 0);
+  };
+  auto form_y = [&](v16i (&acc)[2], float (&y)[2][16], int k) {
+    const float sr = sal[((k & 1) * 8 + wave) * 64 + lane];
+    float am = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int c = 64 * wave + 32 * u + 16 * hh + 4 * qq;
+        const float4 s4 = *reinterpret_cast<const float4*>(swl + c);
+        const float4 b4 = *reinterpret_cast<const float4*>(swl + 512 + c);
+        const float swq[4] = {s4.x, s4.y, s4.z, s4.w}, bq4[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          y[u][4 * qq + e] = fmaxf(((float)acc[u][4 * qq + e] * sr) * swq[e] + bq4[e], 0.0f);
+          am = fmaxf(am, y[u][4 * qq + e]);
+        }
+      }
+    am = fmaxf(am, __shfl_xor(am, 32));
+    if (lane < 32) redb(k)[wave * WP_R + lane] = am;
+  };
+  auto slice_max = [&](int k) {
+    const float* red = redb(k);
+    float m = red[tok];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w * WP_R + tok]);
+    return m;
+  };
+  auto gidx = [&](int rb, int tt) { return ((long)rb * 4 + tt) * 32 + tok; };
+  auto publish = [&](int k, float m) {
+    if (wave == 0 && lane < 32 && t != g.drop_slice)
+      __hip_atomic_store(gran + gidx(rbk(k), t), (1ull << 32) | __float_as_uint(m),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  const unsigned lim = (unsigned)g.spin_limit;
+  auto full_max = [&](int k, float mloc) {
+    const int rb = rbk(k);
+    float m = mloc;
+    for (unsigned spin = 0;; ++spin) {
+      bool ok = true;
+      float mx = mloc;
+#pragma unroll
+      for (int d = 1; d < 4; ++d) {
+        const unsigned long long v = __hip_atomic_load(gran + gidx(rb, (t + d) & 3), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        ok &= (v >> 32) == 1ull;
+        mx = fmaxf(mx, __uint_as_float((unsigned)v));
+      }
+      if (__all(ok)) { m = mx; break; }
+      if (spin >= lim) {                            // bounded: never hang, never silent
+        if (lane == 0)
+          __hip_atomic_fetch_or(g.status, DEV_E_EXCHANGE_TIMEOUT, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    return m;
+  };
+  auto scales = [&](int k, float& bq, float& iq) {
+    const float* gs = gsc + (k & 1) * 2 * WP_R;
+    bq = gs[tok];
+    iq = gs[WP_R + tok];
+  };
+  auto store_tile = [&](int k, int u, const uint32_t (&d)[4]) {
+    const long row = rbk(k) * WP_R + tok;
+    __builtin_amdgcn_raw_buffer_store_b128(v4u{d[0], d[1], d[2], d[3]}, orsrc,
+                                           (int)kp_off(row, c0 + 32 * u, g.ldo8), 0, 0);
+  };
+  auto quant_all = [&](int k, const float (&y)[2][16]) {      // 2 stores (+ wave 0's scale)
+    float bq, iq;
+    scales(k, bq, iq);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      uint32_t d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        d[j] = pack4_biased(rint_biased(div_cr(y[u][4 * j], bq, iq)),
+                            rint_biased(div_cr(y[u][4 * j + 1], bq, iq)),
+                            rint_biased(div_cr(y[u][4 * j + 2], bq, iq)),
+                            rint_biased(div_cr(y[u][4 * j + 3], bq, iq)));
+      store_tile(k, u, d);
+    }
+  };
+  auto mfma_block = [&](v16i (&acc)[2], int k, auto q_c, int kq, float (&y)[2][16]) {
+    constexpr bool Q = decltype(q_c)::value;
+    const uint8_t* cur = lds + (k & 1) * WP_STAGE;
+    float bq = 0.0f, iq = 0.0f;
+    if constexpr (Q) scales(kq, bq, iq);
+    float hist = 0.0f, tq[4];
+    uint32_t d[4];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const v4i x = *reinterpret_cast<const v4i*>(cur + (s << 10) + lane * 16);
+      v4i w[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        w[u] = s < W32_SR ? wr[s < W32_SR ? s : 0][u]
+                          : *reinterpret_cast<const v4i*>(wl + (((wave * (16 - W32_SR) + s - W32_SR) * 2 + u) << 10) + lane * 16);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if constexpr (!Q) {
+          if (s == 0) mfma32_asm<true>(acc[u], w[u], x);
+          else mfma32_asm<false>(acc[u], w[u], x);
+        } else {
+          const int o = 2 * s + u, uo = o >> 4, r = o & 15;
+          float yv = y[uo][r];
+          if (s == 0) mfma32_pin<true>(acc[u], w[u], x, hist, yv);
+          else mfma32_pin<false>(acc[u], w[u], x, hist, yv);
+          tq[r & 3] = rint_biased(div_cr(yv, bq, iq));
+          hist = tq[r & 3];
+          if ((r & 3) == 3) {
+            d[r >> 2] = pack4_biased(tq[0], tq[1], tq[2], tq[3]);
+            if (r == 15) store_tile(kq, uo, d);
+          }
+        }
+      }
+    }
+    mfma32_settle(acc);
+    if constexpr (!Q) dummy_stores();
+  };
+  const std::true_type T_{};
+  const std::false_type F_{};
+
+  v16i acc[2];
+  float y0[2][16], y1[2][16];      // y of the even / odd blocks
+  float mq0 = 0.0f, mq1 = 0.0f;    // their slice maxima
+  __builtin_amdgcn_s_waitcnt(WAIT_VM(0));
+  __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+  __builtin_amdgcn_s_barrier();
+  auto iter = [&](int k, float (&yb)[2][16], float& mb, float& mo) {
+    if (k > 0) {
+      __builtin_amdgcn_s_waitcnt(WAIT_VM(0));   // block k's DMA and the 3 stores after it (VM_CNT_ORDER)
+      __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+      __builtin_amdgcn_s_barrier();
+    }
+    if (wave == 0 && k >= 1 && k <= nblk) {     // only wave 0 publishes and gathers
+      mo = slice_max(k - 1);
+      publish(k - 1, mo);
+    }
+    if (k + 1 < nblk) issue(k + 1);
+    if (k < nblk) {
+      if (k >= 2) mfma_block(acc, k, T_, k - 2, yb);
+      else mfma_block(acc, k, F_, 0, yb);
+      form_y(acc, yb, k);
+    } else if (k >= 2) {
+      quant_all(k - 2, yb);
+    } else {
+      dummy_stores();
+    }
+    if (wave == 0 && k >= 1 && k <= nblk) {
+      const float m = full_max(k - 1, mo);
+      const float sc = fmaxf(m, 1e-5f) / 127.0f;
+      const float inv = 1.0f / sc;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc), srsrc, 4 * (rbk(k - 1) * WP_R + tok), 0, 0);
+      if (lane < WP_R) {
+        float* gs = gsc + ((k - 1) & 1) * 2 * WP_R;
+        gs[lane] = sc;
+        gs[WP_R + lane] = inv;
+      }
+    }
+  };
+  for (int k = 0; k <= nblk + 1; k += 2) {
+    iter(k, y0, mq0, mq1);
+    if (k + 1 <= nblk + 1) iter(k + 1, y1, mq1, mq0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// W [N, 512] row-major -> the WS32 layout (k_gemm_wsq32): one thread per 16-byte chunk.
+__global__ void k_pack_w_ws32(const int8_t* W, int N, int8_t* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;   // output chunk index
+  if (i >= (long)N * 32) return;
+  const int lane = (int)(i & 63), u = (int)((i >> 6) & 1), s = (int)((i >> 7) & 15);
+  const int w = (int)((i >> 11) & 7), t = (int)(i >> 14);
+  const int r = lane & 31;
+  const long n = 512L * t + 64 * w + 32 * u + 16 * ((r >> 2) & 1) + 4 * (r >> 3) + (r & 3);
+  *reinterpret_cast<uint4*>(out + 16 * i) =
+      *reinterpret_cast<const uint4*>(W + n * WS_K + 32 * s + 16 * (lane >> 5));
+}
+hipError_t launch_pack_w_ws32(const int8_t* W, int N, int K, int8_t* out, hipStream_t st) {
+  if (N % 512 || N <= 0 || K != WS_K) return hipErrorInvalidValue;
+  const long nch = (long)N * 32;
+  k_pack_w_ws32<<<dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, st>>>(W, N, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm_ws32_diag(const RowGemmArgs& g, dim3 grid, hipStream_t st) {
+  if (g.epi != RE_QUANT) return hipErrorInvalidValue;
+  if (knobs().ws32 == 2) k_gemm_wsq32<1, 16><<<grid, dim3(512), 0, st>>>(g);   // all of W in VGPRs
+  else k_gemm_wsq32<<<grid, dim3(512), 0, st>>>(g);
+  return hipGetLastError();
+}
+hipError_t launch_gemm_wsy32_diag(const RowGemmArgs& a, int ng, hipStream_t st) {
+  k_gemm_wsy32<<<dim3(4 * 8 * ng), dim3(512), 0, st>>>(a);
+  return hipGetLastError();
+}
+
 hipError_t launch_gemm_ws_diag(const RowGemmArgs& g, dim3 grid, hipStream_t st) {
   const Knobs& kn = knobs();
   if (g.epi == RE_QUANT) {
@@ -1417,3 +1936,8 @@ hipError_t launch_gemm_wsx_diag(const RowGemmArgs& a, int ng, hipStream_t st) {
 }
 
 }  // namespace qtx
+
+// W [N, 512] -> the WS32 layout, for tests/diag_variants.py (diagnostic library only)
+extern "C" int qtx_debug_pack_w_ws32(const int8_t* W, int N, int K, int8_t* out, void* st) {
+  return (int)qtx::launch_pack_w_ws32(W, N, K, out, (hipStream_t)st);
+}

@@ -20,9 +20,25 @@
 
 using namespace qtx;
 
+#ifdef QTX_DIAG
+namespace qtx {   // csrc/diag/qtx_wsgemm_diag.hip
+hipError_t launch_pack_w_ws32(const int8_t* W, int N, int K, int8_t* out, hipStream_t st);
+}
+#endif
+
 namespace {
 
 thread_local std::string g_err;
+
+// the WS32 copies exist only in the diagnostic build (qws32 stays null in the product)
+hipError_t pack_w_ws32(const int8_t* W, int N, int K, int8_t* out, hipStream_t st) {
+#ifdef QTX_DIAG
+  return launch_pack_w_ws32(W, N, K, out, st);
+#else
+  (void)W; (void)N; (void)K; (void)out; (void)st;
+  return hipErrorInvalidValue;
+#endif
+}
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -66,7 +82,7 @@ struct QLin {
   int N = 0, K = 0;
   int8_t* qkp = nullptr;   // encoder, 8-bit: q in the row GEMM's KP layout (pack_w_kp)
   int8_t* qws = nullptr;   // encoder, 8-bit, K == 512: q in the weight-stationary order
-  int8_t* qws32 = nullptr; // encoder Q/K/V, FFN1: q in the WS32 order (k_gemm_wsq32 / wsy32)
+  int8_t* qws32 = nullptr; // encoder Q/K/V, FFN1 in the WS32 order (diagnostic build: QTX_WS32)
   // 4-bit models: the int4 values (in [-7, 7]) unpacked to int8 [N, K] once at load, so the
   // int8 kernels run them — exact (integer products), and the decode is latency-bound, so
   // the packed form's half bytes bought nothing while its unpack lengthened every kernel
@@ -344,7 +360,9 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     if (c.d_ff % 512 == 0)   // weight-stationary copies (K = 512 GEMMs)
       for (auto& e : m->enc) {
         for (QLin* L : {&e.qkv, &e.o, &e.w1}) L->qws = ar.take<int8_t>((size_t)L->N * L->K);
+#ifdef QTX_DIAG
         for (QLin* L : {&e.qkv, &e.w1}) L->qws32 = ar.take<int8_t>((size_t)L->N * L->K);
+#endif
       }
     if (c.d_ff % 64 == 0)    // the fused FFN's weight stream (F KB per layer)
       for (auto& e : m->enc) e.ffn = ar.take<int8_t>((size_t)F * 1024);
@@ -424,7 +442,7 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
     for (QLin* L : {&e.qkv, &e.o, &e.w1, &e.w2})
       if ((L->qkp && launch_pack_w_kp(L->w8(), L->N, L->K, L->qkp, st) != hipSuccess) ||
           (L->qws && launch_pack_w_ws(L->w8(), L->N, L->K, L->qws, st) != hipSuccess) ||
-          (L->qws32 && launch_pack_w_ws32(L->w8(), L->N, L->K, L->qws32, st) != hipSuccess)) {
+          (L->qws32 && pack_w_ws32(L->w8(), L->N, L->K, L->qws32, st) != hipSuccess)) {
         qtx_model_destroy(m);
         return fail(QTX_E_HIP, "KP / WS weight pack");
       }
@@ -666,7 +684,7 @@ RowGemmArgs rowgemm(const QLin& L, const int8_t* a8, const float* sa, int M, int
   RowGemmArgs g{};
   const bool ws = kp && L.qws && L.K == 512 &&
                   (epi == RE_RES_LN ? ws_res_ok(M) : M >= ws_min_m());
-  // Q/K/V on the 32x32x32 MFMA kernel (QTX_WS32)
+  // Q/K/V on the 32x32x32 MFMA kernel (diagnostic build, QTX_WS32)
   const bool ws32 = ws && epi == RE_QUANT && L.qws32 && knobs().ws32;
   g.A = a8; g.lda = L.K; g.sa = sa; g.W = ws32 ? L.qws32 : ws ? L.qws : kp ? L.qkp : L.w8();
   g.ldw = L.K;
@@ -1862,14 +1880,6 @@ int32_t qtx_pack_w_ws(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* 
   if (!W || !out) return fail(QTX_E_INVALID, "null argument");
   const hipError_t e = launch_pack_w_ws(W, N, K, out, (hipStream_t)stream);
   if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "pack_w_ws N=%d K=%d", N, K);
-  HIPCHK(e);
-  return QTX_OK;
-}
-
-int32_t qtx_pack_w_ws32(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* stream) {
-  if (!W || !out) return fail(QTX_E_INVALID, "null argument");
-  const hipError_t e = launch_pack_w_ws32(W, N, K, out, (hipStream_t)stream);
-  if (e == hipErrorInvalidValue) return fail(QTX_E_UNSUPPORTED, "pack_w_ws32 N=%d K=%d", N, K);
   HIPCHK(e);
   return QTX_OK;
 }

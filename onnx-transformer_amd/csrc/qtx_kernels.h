@@ -146,9 +146,8 @@ struct RowGemmArgs {
   // kp: A and W in the KP layout (W rows additionally in the per-512-tile LDS column order,
   // pack_w_kp), and the int8 lnq / RELU_QUANT out8 outputs written KP (RE_QUANT outputs
   // stay row-major: attention reads them); no fault support.  2: W in the WS layout
-  // (weight-stationary, launch_gemm_ws); 3: the one-pass FFN1 (launch_gemm_wsx); 4: W in the
-  // WS32 layout (Q/K/V on k_gemm_wsq32, launch_gemm_ws); 5: the one-pass FFN1 with W in the
-  // WS32 layout (k_gemm_wsy32, launch_gemm_wsx)
+  // (weight-stationary, launch_gemm_ws); 3: the one-pass FFN1 (launch_gemm_wsx); 4 / 5: Q/K/V
+  // / the one-pass FFN1 with W in the WS32 layout (k_gemm_wsq32 / wsy32: diagnostic build)
   int kp;
   // k_gemm_wsx (kp = 3): device status word OR-ed with DEV_E_EXCHANGE_TIMEOUT when a wait
   // for the partner slices' row maxima hit its spin bound (that block's codes were then
@@ -177,8 +176,6 @@ hipError_t launch_gemm_ws(const RowGemmArgs& a, hipStream_t st);
 // row maxima exchanged in-launch through the u64 granule array in a.pmax_out (>= 32*M B)
 hipError_t launch_gemm_wsx(const RowGemmArgs& a, hipStream_t st);
 hipError_t launch_pack_w_ws(const int8_t* W, int N, int K, int8_t* out, hipStream_t st);
-// the WS32 layout of k_gemm_wsq32 (Q/K/V on v_mfma_i32_32x32x32_i8; RowGemmArgs kp = 4)
-hipError_t launch_pack_w_ws32(const int8_t* W, int N, int K, int8_t* out, hipStream_t st);
 
 // The encoder's FFN sublayer in one launch (qtx_ffn.hip, k_ffn_fused): FFN1 (+ReLU, per-token
 // quantization of the hidden over all F columns) and FFN2 (+residual, next LayerNorm + quant)

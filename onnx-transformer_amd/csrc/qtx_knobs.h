@@ -33,7 +33,6 @@ struct Knobs {
   long ws_min_m = 2048;      // QTX_WS_MIN_M: weight-stationary from this many rows
   long ws_res_min_m = 2048;  // QTX_WS_RES_MIN_M / _MAX_M: the O-projection's WS range
   long ws_res_max_m = 8192;
-  bool ws32 = false;         // QTX_WS32: Q/K/V on k_gemm_wsq32 (v_mfma_i32_32x32x32_i8)
   bool no_ffn_fused = false; // QTX_NO_FFN_FUSED: the encoder FFN as FFN1 + FFN2 launches
   // QTX_FFN_FUSED_MIN_M: the fused FFN launch from this many rows (default: off — measured
   // slower than the split launches at cfg3, DESIGN.md §4 "The fused FFN kernel")
@@ -61,6 +60,8 @@ struct Knobs {
   int skinny_wide = -1;      // QTX_SKINNY_WIDE
   int rb_i8_512 = 4, rb_ln = 4, rb_i8_2048 = 4, rb_f32q = 4;   // QTX_RB_*
   int skinny8_maxm = 32;     // QTX_SKINNY8_MAXM
+  int ws32 = 0;              // QTX_WS32: Q/K/V + FFN1 on k_gemm_wsq32 / wsy32 (32x32x32 MFMA;
+                             // 2: Q/K/V with all of W in registers)
 };
 
 // the switches, read from the environment on first use

@@ -42,7 +42,6 @@ Knobs read_env() {
   k.ws_res_min_m = num("QTX_WS_RES_MIN_M", 2048L);
   k.ws_res_max_m = num("QTX_WS_RES_MAX_M", 8192L);
   k.status_slots = (int)num("QTX_STATUS_SLOTS", 0);
-  k.ws32 = flag("QTX_WS32");
   k.no_ffn_fused = flag("QTX_NO_FFN_FUSED");
   k.ffn_fused_min_m = num("QTX_FFN_FUSED_MIN_M", 1L << 40);
   k.wsx_spin_limit = (int)num("QTX_WSX_SPIN_LIMIT", -1);
@@ -67,6 +66,7 @@ Knobs read_env() {
   k.rb_i8_2048 = (int)num("QTX_RB_I8_2048", 4);
   k.rb_f32q = (int)num("QTX_RB_F32Q", 4);
   k.skinny8_maxm = (int)num("QTX_SKINNY8_MAXM", 32);
+  k.ws32 = (int)num("QTX_WS32", 0);
 #endif
   return k;
 }

@@ -68,32 +68,16 @@ __device__ __forceinline__ void mfma_settle(v4i (&acc)[2][4]) {
                  "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[1][2]), "+v"(acc[1][3]));
 }
 
-// The same statements for v_mfma_i32_32x32x32_i8 (k_gemm_wsq32): 16 accumulators per lane,
-// 16 passes, so the settle pad is 24 wait states.
-template <bool Z, typename T>
-__device__ __forceinline__ void mfma32_pin(v16i& acc, const v4i& w, const v4i& a, float before, T& after) {
-  if constexpr (Z)
-    asm volatile("v_mfma_i32_32x32x32_i8 %0, %2, %3, 0" : "=&v"(acc), "+v"(after) : "v"(w), "v"(a), "v"(before));
-  else
-    asm volatile("v_mfma_i32_32x32x32_i8 %0, %2, %3, %0" : "+v"(acc), "+v"(after) : "v"(w), "v"(a), "v"(before));
-}
-template <bool Z>
-__device__ __forceinline__ void mfma32_asm(v16i& acc, const v4i& w, const v4i& a) {
-  if constexpr (Z)
-    asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, 0" : "=&v"(acc) : "v"(w), "v"(a));
-  else
-    asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+v"(acc) : "v"(w), "v"(a));
-}
-__device__ __forceinline__ void mfma32_settle(v16i (&acc)[2]) {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc[0]), "+v"(acc[1]));
-}
-
 #ifdef QTX_DIAG
 // qtx_wsgemm_diag.hip (diagnostic build only): the measured-negative weight-stationary
 // variants the knobs select (QTX_WSQ=2/3/4, QTX_WSA2, QTX_WSY=0); hipErrorNotSupported when
 // they select none
 hipError_t launch_gemm_ws_diag(const RowGemmArgs& g, dim3 grid, hipStream_t st);
 hipError_t launch_gemm_wsx_diag(const RowGemmArgs& a, int ng, hipStream_t st);
+// k_gemm_wsq32 / k_gemm_wsy32 (RowGemmArgs kp = 4 / 5: W in the WS32 layout)
+hipError_t launch_gemm_ws32_diag(const RowGemmArgs& g, dim3 grid, hipStream_t st);
+hipError_t launch_gemm_wsy32_diag(const RowGemmArgs& a, int ng, hipStream_t st);
+hipError_t launch_pack_w_ws32(const int8_t* W, int N, int K, int8_t* out, hipStream_t st);
 #endif
 
 }  // namespace qtx

@@ -86,7 +86,6 @@ SIGNATURES = {
     "qtx_linear_rows": (I32, [C.POINTER(RowGemm), P]),
     "qtx_pack_w_kp": (I32, [P, I32, I32, P, P]),
     "qtx_pack_w_ws": (I32, [P, I32, I32, P, P]),
-    "qtx_pack_w_ws32": (I32, [P, I32, I32, P, P]),
     "qtx_ffn_rows": (I32, [C.POINTER(FfnRows), P]),
     "qtx_pack_ffn": (I32, [P, P, I32, P, P]),
     "qtx_pack_int4": (I32, [P, I32, I32, P, P]),

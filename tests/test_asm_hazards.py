@@ -37,10 +37,20 @@ def _asm(tmp_path, src, name, extra=()):
 def test_asm_mfma_wait_states(tmp_path):
     s = _asm(tmp_path, os.path.join(CSRC, "qtx_wsgemm.hip"), "ws")
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools/check_asm_mfma.py"), s,
-                        "k_gemm_wsq", "k_gemm_wsq32", "k_gemm_wsy", "k_gemm_wsy32"], capture_output=True, text=True,
-                       timeout=120)
+                        "k_gemm_wsq", "k_gemm_wsy"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-3000:]
-    for k in ("k_gemm_wsq", "k_gemm_wsq32", "k_gemm_wsy", "k_gemm_wsy32"):
+    for k in ("k_gemm_wsq", "k_gemm_wsy"):
+        assert f"{k}: 0 hazards" in r.stdout, r.stdout[-2000:]
+
+
+@needs_hipcc
+def test_asm_mfma_wait_states_diag(tmp_path):
+    """The diagnostic build's asm-MFMA kernels, the 32x32x32 ones (16-pass results) included."""
+    s = _asm(tmp_path, os.path.join(CSRC, "diag", "qtx_wsgemm_diag.hip"), "wsd", ["-DQTX_DIAG"])
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools/check_asm_mfma.py"), s,
+                        "k_gemm_wsq32", "k_gemm_wsy32"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-3000:]
+    for k in ("k_gemm_wsq32", "k_gemm_wsy32"):
         assert f"{k}: 0 hazards" in r.stdout, r.stdout[-2000:]
 
 

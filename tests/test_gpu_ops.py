@@ -425,40 +425,14 @@ def test_linear_rows_ws_qkv_scales(torch, M):
         np.testing.assert_array_equal(os_[t].cpu().numpy(), s)
 
 
-@pytest.mark.parametrize("M", [300, 7, 20011, 4096, 8160, 32768, 64, 31, 33])
-def test_linear_rows_ws32_qkv_scales(torch, M):
-    """Q/K/V (epi 0) on the 32x32x32-MFMA weight-stationary kernel (kp = 4, k_gemm_wsq32, W
-    by qtx_pack_w_ws32): the same outputs as kp = 2 bit for bit, with row scales from 1e-35
-    to 1e25 and 1..13 blocks per workgroup, ragged last blocks (M = 7 / 31 / 33 / 20011)."""
-    from qtx._lib import lib
-    rng = np.random.default_rng(M + 23)
-    qx, sx = O.quant_rows(rng.standard_normal((M, 512)).astype(f32))
-    sx = (sx * np.float32(10.0) ** rng.integers(-33, 26, M)).astype(f32)
-    qw, sw = O.quant_weight((rng.standard_normal((1536, 512)) * 0.05).astype(f32), 8)
-    b = (rng.standard_normal(1536) * 1e-3).astype(f32)
-    wk = torch.empty((1536, 512), dtype=torch.int8, device="cuda")
-    assert lib().qtx_pack_w_ws32(P(dev(torch, qw)), 1536, 512, P(wk), S0) == 0
-    out8 = torch.empty((3, M, 512), dtype=torch.int8, device="cuda")
-    os_ = torch.empty((3, M), dtype=torch.float32, device="cuda")
-    _rows_call(torch, A=dev(torch, _to_kp(qx)), sa=dev(torch, sx), W=wk, sw=dev(torch, sw),
-               bias=dev(torch, b), M=M, N=1536, K=512, epi=0, out8=out8, ldo8=512,
-               o8_ts=M * 512, os=os_, os_ts=M, kp=4)
-    y = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b)
-    for t in range(3):
-        q, s = O.quant_rows(y[:, 512 * t:512 * (t + 1)])
-        np.testing.assert_array_equal(out8[t].cpu().numpy(), q)
-        np.testing.assert_array_equal(os_[t].cpu().numpy(), s)
-
-
-@pytest.mark.parametrize("M,kp", [(300, 3), (7, 3), (20011, 3), (4096, 3), (64, 3), (32768, 3),
-                                  (300, 5), (7, 5), (20011, 5), (4096, 5), (64, 5), (32768, 5),
-                                  (33, 5)])
-def test_linear_rows_ws_ffn1_onepass_scales(torch, M, kp):
+@pytest.mark.parametrize("M", [300, 7, 20011, 4096, 64, 32768])
+def test_linear_rows_ws_ffn1_onepass_scales(torch, M):
     """FFN1 in one pass (kp = 3: ReLU + per-token quantization over all 2048 columns, the
     4 column slices' row maxima exchanged inside the launch) on k_gemm_wsy (quantization
-    between the MFMAs), and kp = 5 on k_gemm_wsy32 (the 32x32x32 MFMA, W by
-    qtx_pack_w_ws32), with row scales from 1e-35 to 1e25; bit-exact, and the exchange never
-    timed out (status word 0)."""
+    between the MFMAs), with row scales from 1e-35 to 1e25; bit-exact, and the exchange
+    never timed out (status word 0).  (kp = 4 / 5, the 32x32x32-MFMA variants: diagnostic
+    build, tests/diag_variants.py.)"""
+    kp = 3
     from qtx._lib import lib
     wsy = 1
     rng = np.random.default_rng(M + 31 * wsy)
@@ -467,8 +441,7 @@ def test_linear_rows_ws_ffn1_onepass_scales(torch, M, kp):
     qw, sw = O.quant_weight((rng.standard_normal((2048, 512)) * 0.05).astype(f32), 8)
     b = (rng.standard_normal(2048) * 1e-3).astype(f32)
     wk = torch.empty((2048, 512), dtype=torch.int8, device="cuda")
-    pack = lib().qtx_pack_w_ws if kp == 3 else lib().qtx_pack_w_ws32
-    assert pack(P(dev(torch, qw)), 2048, 512, P(wk), S0) == 0
+    assert lib().qtx_pack_w_ws(P(dev(torch, qw)), 2048, 512, P(wk), S0) == 0
     h8 = torch.zeros((M + (M & 1), 2048), dtype=torch.int8, device="cuda")
     sh = torch.full((M,), -1.0, dtype=torch.float32, device="cuda")
     nb = (M + 31) // 32
@@ -559,31 +532,6 @@ def test_pack_w_ws(torch):
     assert lib().qtx_pack_w_ws(P(dev(torch, w)), 1024, 512, P(out), S0) == 0
     np.testing.assert_array_equal(out.cpu().numpy(), _ws_pack_ref(w))
     assert lib().qtx_pack_w_ws(P(dev(torch, w)), 1024, 256, P(out), S0) != 0   # K != 512
-
-
-def _ws32_pack_ref(w):
-    """The WS32 order of qtx_pack_w_ws32 (include/qtx.h), restated in numpy: 1 KB block
-    ((t*8 + w)*16 + s)*2 + u, lane l (r = l & 31): W[512t + 64w + 32u + 16((r >> 2) & 1) +
-    4(r >> 3) + (r & 3)][32s + 16(l >> 5) .. +16]."""
-    N, K = w.shape
-    t, wv, s, u, l = np.meshgrid(np.arange(N // 512), np.arange(8), np.arange(16), np.arange(2),
-                                 np.arange(64), indexing="ij")
-    r = l & 31
-    n = 512 * t + 64 * wv + 32 * u + 16 * ((r >> 2) & 1) + 4 * (r >> 3) + (r & 3)
-    k0 = 32 * s + 16 * (l >> 5)
-    rows = w[n.reshape(-1)]
-    idx = k0.reshape(-1)[:, None] + np.arange(16)[None, :]
-    return np.take_along_axis(rows, idx, axis=1).reshape(N, K)
-
-
-def test_pack_w_ws32(torch):
-    rng = np.random.default_rng(6)
-    w = rng.integers(-127, 128, (1536, 512)).astype(np.int8)
-    out = torch.empty((1536, 512), dtype=torch.int8, device="cuda")
-    from qtx._lib import lib
-    assert lib().qtx_pack_w_ws32(P(dev(torch, w)), 1536, 512, P(out), S0) == 0
-    np.testing.assert_array_equal(out.cpu().numpy(), _ws32_pack_ref(w))
-    assert lib().qtx_pack_w_ws32(P(dev(torch, w)), 1536, 256, P(out), S0) != 0   # K != 512
 
 
 @pytest.mark.parametrize("M,nopipe", [(300, 0), (7, 0), (64, 0), (20011, 0), (20011, 1), (300, 1)])

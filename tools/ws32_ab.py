@@ -1,7 +1,9 @@
 """A/B of Q/K/V and FFN1 on k_gemm_wsq32 / k_gemm_wsy32 (QTX_WS32=1) against k_gemm_wsq / wsy, alternated in ONE process:
 the QKV and FFN1 launches alone at cfg3's M (bench.time_row_gemms) and the whole cfg3 encoder.
 
-    python tools/ws32_ab.py [rounds]
+    QTX_LIB_PATH=onnx-transformer_amd/qtx/libqtx_diag.so python tools/ws32_ab.py [rounds] [variants, e.g. 0,1,2]
+
+(the 32x32x32 kernels are in the diagnostic library only).  Result (round 5): DESIGN.md §4.
 """
 import json
 import os
@@ -19,9 +21,10 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     model = QtxModel(synthetic_state_dict(20241223))
     L = _lib.lib(build=False)
-    res = {"0": [], "1": []}
+    vs = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "2"]
+    res = {v: [] for v in vs}
     for r in range(rounds):
-        for v in ("0", "1"):
+        for v in vs:
             os.environ["QTX_WS32"] = v
             L.qtx_debug_reload_knobs()
             g = bench.time_row_gemms(reps=20)
@@ -29,9 +32,9 @@ def main():
             d = {"qkv_us": round(g["qkv_quant"][0], 2), "ffn1_us": round(g["ffn1_quant_onepass"][0], 2),
                  "encoder_ms": round(enc, 4)}
             res[v].append(d)
-            print(r, "ws32" if v == "1" else "wsq ", json.dumps(d), flush=True)
+            print(r, f"QTX_WS32={v}", json.dumps(d), flush=True)
     for v, runs in res.items():
-        print("BEST", "ws32" if v == "1" else "wsq ", json.dumps({k: min(x[k] for x in runs) for k in runs[0]}))
+        print("BEST", f"QTX_WS32={v}", json.dumps({k: min(x[k] for x in runs) for k in runs[0]}))
 
 
 if __name__ == "__main__":
