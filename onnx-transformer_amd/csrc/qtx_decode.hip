@@ -558,7 +558,7 @@ template <bool KV_NEW, int NIT>
 __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   __shared__ uint32_t Ks[DEC_MAXK * 17];   // key rows of this head: 16 dwords (+1 pad)
   __shared__ __attribute__((aligned(16))) uint8_t Vs[DEC_MAXK * 64];
-  __shared__ float sks[DEC_MAXK], svs[DEC_MAXK], P[DEC_MAXK];
+  __shared__ float svs[DEC_MAXK], P[DEC_MAXK];
   __shared__ __attribute__((aligned(16))) int8_t qs[64];
   const int b = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
   QTX_STAMP(0);
@@ -601,7 +601,7 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
 #endif
   }
   const int j0 = min(lane, nrows - 1), j1 = min(lane + 64, nrows - 1);
-  const float sk0 = a.skc[kvb + j0], sk1 = a.skc[kvb + j1];
+  float sk0 = a.skc[kvb + j0], sk1 = a.skc[kvb + j1];
   const float sv0 = a.svc[kvb + j0], sv1 = a.svc[kvb + j1];
   bool keep0 = true, keep1 = true;
   if constexpr (!KV_NEW) {
@@ -649,12 +649,14 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
     kd[0] = kr[i].x; kd[1] = kr[i].y; kd[2] = kr[i].z; kd[3] = kr[i].w;
     *reinterpret_cast<uint4*>(Vs + r * 64 + 16 * ch) = vr[i];
   }
-  sks[j0] = sk0; sks[j1] = sk1; svs[j0] = sv0; svs[j1] = sv1;
+  svs[j0] = sv0; svs[j1] = sv1;
   __syncthreads();
   if constexpr (KV_NEW) {
     reinterpret_cast<int8_t*>(&Ks[step * 17])[lane] = kq;
     Vs[step * 64 + lane] = (uint8_t)vq;
-    if (lane == 0) { sks[step] = sk; svs[step] = sv; }
+    if (lane == 0) svs[step] = sv;
+    if (lane == step) sk0 = sk;            // the key scales stay in the lane that scores
+    if (lane + 64 == step) sk1 = sk;       // the key (lane + 64 u)
     __syncthreads();
   }
   QTX_STAMP(1);
@@ -663,6 +665,8 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   uint32_t qd[16];
 #pragma unroll
   for (int w = 0; w < 16; ++w) qd[w] = reinterpret_cast<const uint32_t*>(qs)[w];
+  // (the scores and exponentials stay in registers: lane owns keys lane, lane + 64)
+  float sc[2] = {0.0f, 0.0f};
   float lmax = -3.0e38f;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -671,9 +675,9 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
       int acc = 0;
 #pragma unroll
       for (int w = 0; w < 16; ++w) acc = __builtin_amdgcn_sdot4(qd[w], Ks[j * 17 + w], acc, false);
-      float s = (((float)acc * sq) * sks[j]) * 0.125f;
+      float s = (((float)acc * sq) * (u ? sk1 : sk0)) * 0.125f;
       if (!(u ? keep1 : keep0)) s = -1.0e9f;
-      P[j] = s;
+      sc[u] = s;
       lmax = fmaxf(lmax, s);
     }
   }
@@ -683,8 +687,8 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   for (int u = 0; u < 2; ++u) {
     const int j = lane + 64 * u;
     if (j < Sk) {
-      const float e = qexp(P[j] - m);
-      P[j] = e;
+      const float e = qexp(sc[u] - m);
+      sc[u] = e;
       lsum = lsum + e;
     }
   }
@@ -696,7 +700,7 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int j = lane + 64 * u;
-    if (j < Sk) P[j] = div127(rintf(div_cr(P[j], den, rden) * 127.0f));
+    if (j < Sk) P[j] = div127(rintf(div_cr(sc[u], den, rden) * 127.0f));
   }
   __syncthreads();
   QTX_STAMP(2);
