@@ -749,80 +749,89 @@ hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st) {
 }
 
 // =====================================================================================
-// k_generator_mfma: the same canonical chain on the fp32 matrix cores.
-// v_mfma_f32_16x16x4_f32 chained over k = 0..511 (128 instructions, C starts at 0) is
-// bit-for-bit the k-ordered fmaf chain (cdna_hip_programming.md §3 "FP32-input MFMA"),
-// so logits[m, v] = (fma chain of x[m,k] * W[v,k]) + b[v] exactly as the oracle.
-// Block = 16 token rows x 64 vocab columns (4 waves, one 16-column strip each).  A operand
-// = the LayerNormed rows in LDS; B operand = the weight packed at load in MFMA order
-// (k_pack_gen: per strip, per group of 4 k-steps, per lane one float4), so each wave
-// streams its whole 32 KB strip with 32 coalesced 1 KB loads issued before the LayerNorm.
-// The two 16-row blocks of a strip group run on one XCD (blockIdx remap): the second
-// reads the strip from that XCD's L2.
+// k_generator_mfma: the canonical generator order on the fp32 matrix cores.
+// logits[m, v] = ((c0 + c1) + (c2 + c3)) + b[v] with c_q the k-ordered fma chain over
+// k in [128q, 128q + 128) from 0 (oracle OracleModel.logits): v_mfma_f32_16x16x4_f32 chained
+// over a quarter (32 instructions, C starting at 0) is bit-for-bit that chain
+// (cdna_hip_programming.md §3 "FP32-input MFMA").
+// Block = 16 token rows x 64 vocab columns, 16 waves: wave w takes strip w & 3 (16
+// columns) and k-quarter w >> 2, so the dependent MFMA chain per wave is 32 long (a lone
+// 128-long chain cost ~6,100 cycles, ~48 per dependent MFMA: tools/stamp_bench.py).  A
+// operand = the LayerNormed rows in LDS (one row per wave); B operand = the weight packed at
+// load in MFMA order (k_pack_gen: per strip, per group of 4 k-steps, per lane one float4),
+// each wave streaming its quarter strip (8 KB) with 8 coalesced 1 KB loads issued before
+// the LayerNorm.  The quarters' partial tiles meet in LDS; the waves of quarter 0 add them
+// in the canonical order and store.  The two 16-row blocks of a strip group run on one XCD
+// (blockIdx remap): the second reads the strips from that XCD's L2.
 // =====================================================================================
 constexpr int GEN_Q = 32;   // float4 groups of 4 k-steps per lane (K = 512)
 
-__global__ __launch_bounds__(256) void k_generator_mfma(const float* x, long ldx, int M,
-                                                        const float* ln_a, const float* ln_b,
-                                                        const float* Wm, const float* bias,
-                                                        int V, float* logits) {
+__global__ __launch_bounds__(1024) void k_generator_mfma(const float* x, long ldx, int M,
+                                                         const float* ln_a, const float* ln_b,
+                                                         const float* Wm, const float* bias,
+                                                         int V, float* logits) {
   __shared__ __attribute__((aligned(16))) float X[16][514];   // stride 514: conflict-free reads
+  __shared__ __attribute__((aligned(16))) v4f part[3][4][64];  // quarters 1..3: [strip][lane]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
+  const int sw = wave & 3, qq = wave >> 2;          // strip within the group, k-quarter
   // blockIdx -> (strip group g, row block rb): hw = 8 (nrb (g / 8) + rb) + g % 8, so the
   // row blocks of group g share hw % 8 (one XCD under round-robin placement)
   const int nrb = (M + 15) / 16, hw = blockIdx.x;
   const int rb = (hw >> 3) % nrb, g = ((hw >> 3) / nrb) * 8 + (hw & 7);
-  const int nstrip = (V + 15) / 16, strip = g * 4 + wave;
+  const int nstrip = (V + 15) / 16, strip = g * 4 + sw;
   if (g * 4 >= nstrip) return;                     // whole block (uniform)
   const int m0 = rb * 16;
   const int vcol = strip * 16 + fr;
   QTX_STAMP(0);
-  // 1. the strip's B operands, all in flight before anything else
-  const float4* wp = reinterpret_cast<const float4*>(Wm) + ((long)min(strip, nstrip - 1) * GEN_Q) * 64 + lane;
-  float4 wq[GEN_Q];
+  // 1. the quarter strip's B operands, all in flight before anything else
+  constexpr int QQ = GEN_Q / 4;
+  const float4* wp = reinterpret_cast<const float4*>(Wm) +
+                     ((long)min(strip, nstrip - 1) * GEN_Q + QQ * qq) * 64 + lane;
+  float4 wq[QQ];
 #pragma unroll
-  for (int q = 0; q < GEN_Q; ++q) wq[q] = wp[q * 64];
+  for (int q = 0; q < QQ; ++q) wq[q] = wp[q * 64];
   const float bv = bias[min(vcol, V - 1)];
-  // 2. 16 rows (4 per wave), LayerNorm in the canonical order, into LDS
-  float xv[4][2][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int m = min(m0 + wave + 4 * j, M - 1);
+  // 2. row `wave` of the block, LayerNorm in the canonical order, into LDS
+  float xv[1][2][4];
+  {
+    const int m = min(m0 + wave, M - 1);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const float4 t = *reinterpret_cast<const float4*>(x + (long)m * ldx + 4 * (lane + 64 * c));
-      xv[j][c][0] = t.x; xv[j][c][1] = t.y; xv[j][c][2] = t.z; xv[j][c][3] = t.w;
+      xv[0][c][0] = t.x; xv[0][c][1] = t.y; xv[0][c][2] = t.z; xv[0][c][3] = t.w;
     }
   }
-  if (ln_a) ln_rows512<4>(xv, ln_a, ln_b, lane);
+  if (ln_a) ln_rows512<1>(xv, ln_a, ln_b, lane);
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      float* d = &X[wave + 4 * j][4 * (lane + 64 * c)];
-      *reinterpret_cast<float2*>(d) = make_float2(xv[j][c][0], xv[j][c][1]);
-      *reinterpret_cast<float2*>(d + 2) = make_float2(xv[j][c][2], xv[j][c][3]);
-    }
+  for (int c = 0; c < 2; ++c) {
+    float* d = &X[wave][4 * (lane + 64 * c)];
+    *reinterpret_cast<float2*>(d) = make_float2(xv[0][c][0], xv[0][c][1]);
+    *reinterpret_cast<float2*>(d + 2) = make_float2(xv[0][c][2], xv[0][c][3]);
+  }
   __syncthreads();
   QTX_STAMP(1);
-  // 3. the k-ordered chain: step s = 4q + e uses A = X[fr][4s + fg], B = wq[q][e]
+  // 3. the quarter's k-ordered chain: step s = 4 (QQ qq + q) + e uses A = X[fr][4s + fg],
+  //    B = wq[q][e]
   v4f acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-  for (int q = 0; q < GEN_Q; ++q) {
+  for (int q = 0; q < QQ; ++q) {
     const float b4[4] = {wq[q].x, wq[q].y, wq[q].z, wq[q].w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float a = X[fr][4 * (4 * q + e) + fg];
+      const float a = X[fr][4 * (4 * (QQ * qq + q) + e) + fg];
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b4[e], acc, 0, 0, 0);
     }
   }
+  if (qq) part[qq - 1][sw][lane] = acc;
+  __syncthreads();
   QTX_STAMP(2);
-  if (vcol >= V) return;
+  if (qq || vcol >= V) return;
+  const v4f p1 = part[0][sw][lane], p2 = part[1][sw][lane], p3 = part[2][sw][lane];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int m = m0 + 4 * fg + e;
-    if (m < M) logits[(long)m * V + vcol] = acc[e] + bv;
+    if (m < M) logits[(long)m * V + vcol] = ((acc[e] + p1[e]) + (p2[e] + p3[e])) + bv;
   }
   QTX_STAMP(3);
 }
@@ -833,7 +842,7 @@ hipError_t launch_generator_mfma(const float* x, long ldx, int M, const float* l
   if (M <= 0) return hipSuccess;
   const int ngroup = (V + 63) / 64, nrb = (M + 15) / 16;
   const unsigned grid = 8u * nrb * ((ngroup + 7) / 8);
-  k_generator_mfma<<<dim3(grid), dim3(256), 0, st>>>(x, ldx, M, ln_a, ln_b, Wm, b, V, logits);
+  k_generator_mfma<<<dim3(grid), dim3(1024), 0, st>>>(x, ldx, M, ln_a, ln_b, Wm, b, V, logits);
   return hipGetLastError();
 }
 

@@ -397,7 +397,8 @@ hipError_t launch_embed(const int64_t* ids, long ids_bs, int B, int T, const int
 }
 
 // =====================================================================================
-// k_generator: logits[m, v] = (fma chain over k of x[m,k] * W[v,k]) + b[v].
+// k_generator: logits[m, v] = ((c0 + c1) + (c2 + c3)) + b[v], c_q = the fma chain of
+// x[m,k] * W[v,k] over k in [128q, 128q + 128) from 0 (the oracle's canonical order).
 // Block = 64 vocab rows x 32 token rows; W chunk transposed in LDS.
 // =====================================================================================
 __global__ __launch_bounds__(256) void k_generator(const float* x, long ldx, int M,
@@ -407,10 +408,14 @@ __global__ __launch_bounds__(256) void k_generator(const float* x, long ldx, int
   __shared__ float X[32][64];
   const int tid = threadIdx.x, v = tid & 63, mg = tid >> 6;
   const int v0 = blockIdx.x * 64, m0 = blockIdx.y * 32;
-  float acc[8];
+  float acc[8], part[3][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
   for (int k0 = 0; k0 < 512; k0 += 64) {
+    if (k0 && (k0 & 127) == 0) {            // a new k-quarter: its chain starts from 0
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { part[(k0 >> 7) - 1][i] = acc[i]; acc[i] = 0.0f; }
+    }
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int idx = tid + 256 * p, vv = idx >> 4, kq = idx & 15;
@@ -441,7 +446,7 @@ __global__ __launch_bounds__(256) void k_generator(const float* x, long ldx, int
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + mg + 4 * i;
-    if (m < M) logits[(long)m * V + gv] = acc[i] + bv;
+    if (m < M) logits[(long)m * V + gv] = ((part[0][i] + part[1][i]) + (part[2][i] + acc[i])) + bv;
   }
 }
 

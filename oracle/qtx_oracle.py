@@ -11,7 +11,8 @@ fp32 graphs on ONNXRuntime-CPU; here it is restated as exact intege
 The canonical order is the contract the HIP kernels implement, so the GPU path and this
 oracle agree bit-for-bit (see DESIGN.md §3 "numerics contract"):
 
-* no FMA contraction except where the canonical order says ``fma`` (PV and generator dots);
+* no FMA contraction except where the canonical order says ``fma`` (PV and generator dots;
+  the generator's dot as four partial chains over k-quarters, summed pairwise);
 * LayerNorm / softmax / log-softmax sums use a fixed lane-split + xor-butterfly tree;
 * softmax uses :func:`qexp`, a fixed polynomial exp that both sides evaluate identically.
 
@@ -521,12 +522,19 @@ class OracleModel:
         return (e + self.pe[pos0:pos0 + ids.shape[1]][None]).astype(f32)
 
     def logits(self, x):
-        """proj(x) of generator.py:15: sequential fma chain over k from 0, then + bias."""
+        """proj(x) of generator.py:15 in the canonical order: four partial fma chains, chain q
+        sequential over k in [128q, 128q + 128) from 0, summed as ((c0 + c1) + (c2 + c3)),
+        then + bias (round 5: the four chains run on four waves, qtx_decode.hip
+        k_generator_mfma; the reference's fp32 Linear sums in MLAS order, pinned within 1e-5
+        by tests/test_oracle_golden.py)."""
         x = np.asarray(x, f32)
-        acc = np.zeros((x.shape[0], self.gen_w.shape[0]), f32)
-        for k in range(x.shape[1]):
-            acc = fma32(x[:, k, None], self.gen_w[None, :, k], acc)
-        return (acc + self.gen_b).astype(f32)
+        K = x.shape[1]
+        kq = K // 4
+        acc = [np.zeros((x.shape[0], self.gen_w.shape[0]), f32) for _ in range(4)]
+        for q in range(4):
+            for k in range(q * kq, (q + 1) * kq):
+                acc[q] = fma32(x[:, k, None], self.gen_w[None, :, k], acc[q])
+        return (((acc[0] + acc[1]) + (acc[2] + acc[3])) + self.gen_b).astype(f32)
 
     def generator(self, x):
         """Generator.forward (generator.py:14-15) + first-index argmax
