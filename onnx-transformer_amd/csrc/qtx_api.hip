@@ -129,6 +129,10 @@ struct qtx_model {
   const float* dec_norm[2];
   const float *src_lut, *tgt_lut, *pe, *gen_w, *gen_b;
   float* gen_wt = nullptr;   // generator weight in k_generator_mfma's MFMA order (pack_gen)
+  // the decoder layers' cross K/V linears as ONE [n_layers * 2 * d_model, d_model] linear
+  // (each dec[l].ckv is a view of rows 2 d_model l ..): the once-per-decode cross K/V of all
+  // layers in one launch instead of n_layers (cross_kv)
+  QLin ckv_all;
   void* mem = nullptr;
   size_t bytes = 0;
   // decode-step graphs, keyed by shape and the buffers baked into them
@@ -366,8 +370,20 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
       }
     if (c.d_ff % 64 == 0)    // the fused FFN's weight stream (F KB per layer)
       for (auto& e : m->enc) e.ffn = ar.take<int8_t>((size_t)F * 1024);
+    lin(m->ckv_all, NL * 2 * D, D);
+    for (int l = 0; l < NL; ++l) {   // dec[l].ckv: rows 2Dl .. 2D(l+1) of ckv_all
+      QLin& v = m->dec[l].ckv;
+      const QLin& a = m->ckv_all;
+      v.N = 2 * D; v.K = D;
+      if (a.q) {
+        v.q = a.q + wbytes(c, 2 * D, D) * l;
+        v.q8 = a.q8 ? a.q8 + (size_t)2 * D * D * l : nullptr;
+        v.s = a.s + 2 * D * l;
+        v.b = a.b + 2 * D * l;
+      }
+    }
     for (auto& d : m->dec) {
-      lin(d.qkv, 3 * D, D); lin(d.o, D, D); lin(d.cq, D, D); lin(d.ckv, 2 * D, D);
+      lin(d.qkv, 3 * D, D); lin(d.o, D, D); lin(d.cq, D, D);
       lin(d.co, D, D); lin(d.w1, F, D); lin(d.w2, D, F);
     }
     float* norms = ar.take<float>((size_t)2 * D * (5 * NL + 2));
@@ -1060,11 +1076,15 @@ CrossKV carve_cross(Arena& ar, const qtx_config& c, long Ms) {
   x.am8 = ar.take<int8_t>(Ms * D);
   x.sam = ar.take<float>(Ms);
   x.y = ar.take<float>(Ms * 2 * D);
-  for (int l = 0; l < c.n_layers; ++l) {      // k8|v8 and sk|sv contiguous per layer
-    int8_t* kv = ar.take<int8_t>(2 * Ms * D);
-    float* sc = ar.take<float>(2 * Ms);
-    x.k8.push_back(kv); x.v8.push_back(kv + Ms * D);
-    x.sk.push_back(sc); x.sv.push_back(sc + Ms);
+  // k8 / v8 of every layer contiguous (tile t = 2 l + {0: K, 1: V} at t * Ms * D), and
+  // sk / sv likewise (t * Ms): the layout of one row GEMM's per-512-column-tile outputs
+  int8_t* kv = ar.take<int8_t>(2L * c.n_layers * Ms * D);
+  float* sc = ar.take<float>(2L * c.n_layers * Ms);
+  for (int l = 0; l < c.n_layers; ++l) {
+    x.k8.push_back(kv ? kv + 2L * l * Ms * D : nullptr);
+    x.v8.push_back(kv ? kv + (2L * l + 1) * Ms * D : nullptr);
+    x.sk.push_back(sc ? sc + 2L * l * Ms : nullptr);
+    x.sv.push_back(sc ? sc + (2L * l + 1) * Ms : nullptr);
   }
   return x;
 }
@@ -1075,6 +1095,15 @@ int cross_kv(const qtx_model* m, const float* memory, int Ms, CrossKV& x, hipStr
   const qtx_config& c = m->cfg;
   const int D = c.d_model;
   RC(quant(memory, D, Ms, D, x.am8, x.sam, st));
+  bool ckv_fault = false;
+  for (int l = 0; l < c.n_layers; ++l) ckv_fault |= fault_for(f, 1, l, G_CKV, Ms, c).kind != FK_NONE;
+  if (row_path(c) && D == 512 && !ckv_fault) {
+    // every layer's K and V in ONE row GEMM (N = n_layers * 2 * 512): its 512-column tiles
+    // are the layers' K / V, each quantized per token in the epilogue exactly as the
+    // per-layer launches below (decode prologue: 6 launches of 36 workgroups -> one of 216)
+    RC(row_quant(m->ckv_all, x.am8, x.sam, Ms, x.k8[0], x.sk[0], st));
+    return QTX_OK;
+  }
   for (int l = 0; l < c.n_layers; ++l) {
     if (row_path(c)) {     // K and V tiles quantized in the GEMM epilogue
       RC(row_quant(m->dec[l].ckv, x.am8, x.sam, Ms, x.k8[l], x.sk[l], st,
