@@ -713,9 +713,11 @@ hipError_t launch_row_gemm_any(const RowGemmArgs& g, hipStream_t st) {
 }
 // out = per-token quantized (a8 . W^T) per 512-wide tile into out8 + t*M*512, os + t*M
 int row_quant(const QLin& L, const int8_t* a8, const float* sa, int M, int8_t* out8,
-              float* os, hipStream_t st, const FaultArgs& fa = FaultArgs{}, bool kp = false) {
+              float* os, hipStream_t st, const FaultArgs& fa = FaultArgs{}, bool kp = false,
+              void* zero = nullptr, long zero16 = 0) {
   RowGemmArgs g = rowgemm(L, a8, sa, M, RE_QUANT, kp);
   g.fault = fa;
+  g.zero = zero; g.zero16 = zero16;   // a side job (launch_gemm_ws), else a zeroing kernel
   g.out8 = out8; g.ldo8 = 512; g.o8_ts = (long)M * 512; g.os = os; g.os_ts = M;
   HIPCHK(launch_row_gemm_any(g, st));
   return QTX_OK;
@@ -744,12 +746,21 @@ int row_res_ln(const QLin& L, const int8_t* a8, const float* sa, int M, float* x
 // FFN1 in one weight-stationary pass with the row maxima exchanged between the column
 // slices' workgroups inside the launch (k_gemm_wsx); QTX_NO_WSX=1: the two passes
 bool wsx_on() { return !knobs().no_wsx; }
+// Whether row_ffn1 takes the one-pass FFN1 (k_gemm_wsx / wsy) with its exchange scratch in
+// s.y: then the layer's Q/K/V launch can zero that scratch as a side job (encoder_run).
+bool ffn1_onepass(const QLin& L, int M, bool kp, const FaultArgs& fa) {
+  return rowgemm(L, nullptr, nullptr, M, RE_RELU_PMAX, kp).kp == 2 && L.N == 2048 &&
+         fa.kind == FK_NONE && wsx_on();
+}
+long ffn1_scratch16(int M) { return (4L * 32 * ((M + 31) / 32) + 2) / 2; }   // 16-B chunks
 int row_ffn1(const qtx_config& c, const QLin& L, const int8_t* a8, const float* sa, int M,
              Scratch& s, hipStream_t st,
-             const FaultArgs& fa = FaultArgs{}, bool kp = false, unsigned* status = nullptr) {
+             const FaultArgs& fa = FaultArgs{}, bool kp = false, unsigned* status = nullptr,
+             bool prezeroed = false) {
   RowGemmArgs g = rowgemm(L, a8, sa, M, RE_RELU_PMAX, kp);
   if (g.kp == 2 && L.N == 2048 && fa.kind == FK_NONE && wsx_on()) {
     g.epi = RE_RELU_QUANT_PMAX;
+    g.prezeroed = prezeroed;
     if (L.qws32 && knobs().ws32) { g.W = L.qws32; g.kp = 5; }   // k_gemm_wsy32
     g.pmax_out = s.y;                // granules + ticket: <= 32 * M + 2048 bytes of the (unused) fp32 GEMM scratch
     g.out8 = s.h8; g.ldo8 = c.d_ff; g.os = s.sh;
@@ -993,7 +1004,11 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
   for (int l = 0; l < NL; ++l) {
     const EncLayer& L = m->enc[l];
     auto fa = [&](GemmId gid) { return fault_for(f, 0, l, gid, M, c); };
-    RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st, fa(G_QKV), kp));
+    // the FFN1 below in one pass: its exchange scratch (in s.y, which nothing between here
+    // and it writes) zeroed by the Q/K/V launch instead of a kernel of its own
+    const bool zero_ffn1 = kp && !ffn_fused_ok(L, M, kp) && ffn1_onepass(L.w1, M, kp, fa(G_FFN1));
+    RC(row_quant(L.qkv, s.a8, s.sa, M, s.q8, s.sq, st, fa(G_QKV), kp,
+                 zero_ffn1 ? s.y : nullptr, zero_ffn1 ? ffn1_scratch16(M) : 0));
     if (l == 0 && after_first) HIPCHK(hipEventRecord(after_first, st));
     AttnArgs a = attn_args(s, B, S, S, S);
     a.mask = mask; a.m_bs = S; a.m_is = 0;
@@ -1029,7 +1044,7 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
       HIPCHK(launch_ffn_fused(g, st));
       continue;
     }
-    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1), kp, s.status));
+    RC(row_ffn1(c, L.w1, s.a8, s.sa, M, s, st, fa(G_FFN1), kp, s.status, zero_ffn1));
     if (l + 1 < NL)
       RC(row_res_ln(L.w2, s.h8, s.sh, M, s.x, m->enc[l + 1].ln[0], s.a8, s.sa, nullptr, st,
                     fa(G_FFN2), kp, s.y));

@@ -162,6 +162,12 @@ struct RowGemmArgs {
   // row sums them and runs the residual + LayerNorm + quant epilogue.  0 / 1: no split.
   int32_t* part;
   int ksplit;
+  // side job of the Q/K/V launch (k_gemm_wsq, encoder): zero `zero16` 16-byte chunks at
+  // `zero` — the next one-pass FFN1's exchange scratch (granules, ticket) — so that launch
+  // needs no zeroing kernel of its own (prezeroed).  0: none.
+  void* zero;
+  long zero16;
+  int prezeroed;   // kp = 3: the exchange scratch is already zero (launch_gemm_wsx)
 };
 enum : unsigned { DEV_E_EXCHANGE_TIMEOUT = 1u };
 // W [N, K] int8 row-major -> KP layout with the row GEMM's column permutation per 512-wide

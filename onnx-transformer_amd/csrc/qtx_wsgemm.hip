@@ -681,6 +681,14 @@ __global__ __launch_bounds__(512) void k_gemm_wsq(RowGemmArgs g) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int f = lane & 15, gq = lane >> 4;
   const long long rt_entry = QTX_RNOW();          // QTX_STAMPS builds: kernel entry
+  // the side job (before any early exit): this workgroup's share of the next FFN1's
+  // exchange scratch, zeroed (the stores retire under the prologue's vmcnt(0))
+  if (g.zero16 > 0) {
+    const long per = (g.zero16 + gridDim.x - 1) / gridDim.x;
+    const long z0 = per * blockIdx.x, z1 = min(z0 + per, g.zero16);
+    uint4* zp = reinterpret_cast<uint4*>(g.zero);
+    for (long i = z0 + tid; i < z1; i += 512) zp[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
   const int nsl = g.N >> 9;
   const int wpt = gridDim.x / nsl;
   int t = blockIdx.x % nsl, r0 = blockIdx.x / nsl;
@@ -1438,8 +1446,11 @@ hipError_t launch_gemm_wsx(const RowGemmArgs& g, hipStream_t st) {
   // u64 granules + the ticket counter (padded: a memset of a multiple of 16 bytes), zeroed
   // before every launch
   const long ngran = 4L * 32 * nb + 2;
-  hipError_t e = launch_zero(g.pmax_out, (size_t)ngran * 8, st);   // (a kernel: graph-capturable)
-  if (e != hipSuccess) return e;
+  hipError_t e = hipSuccess;
+  if (!g.prezeroed) {   // (the encoder's Q/K/V launch zeroes it as a side job: prezeroed)
+    e = launch_zero(g.pmax_out, (size_t)ngran * 8, st);   // (a kernel: graph-capturable)
+    if (e != hipSuccess) return e;
+  }
   RowGemmArgs a = g;
   if (!a.status)                              // the u32 after the ticket counter
     a.status = reinterpret_cast<unsigned*>(g.pmax_out) + 2 * (4L * 32 * nb) + 1;
@@ -1467,7 +1478,21 @@ hipError_t launch_gemm_wsx(const RowGemmArgs& g, hipStream_t st) {
   return hipGetLastError();
 }
 
+hipError_t launch_gemm_ws_(const RowGemmArgs& g, hipStream_t st);
+// The zeroing side job (RowGemmArgs::zero) runs inside the product's Q/K/V kernel; any other
+// kernel this call selects gets the zeroing kernel first.
 hipError_t launch_gemm_ws(const RowGemmArgs& g, hipStream_t st) {
+  if (g.zero16 <= 0) return launch_gemm_ws_(g, st);
+  const Knobs& kn = knobs();
+  const bool in_wsq = g.M > 0 && g.epi == RE_QUANT && g.kp == 2 && g.pmax_n <= 4 &&
+                      !kn.ws_nopipe && kn.wsq == 1 && !kn.ws_prio && kn.ws_xg;
+  if (in_wsq) return launch_gemm_ws_(g, st);
+  if (const hipError_t e = launch_zero(g.zero, (size_t)g.zero16 * 16, st); e != hipSuccess) return e;
+  RowGemmArgs a = g;
+  a.zero = nullptr; a.zero16 = 0;
+  return launch_gemm_ws_(a, st);
+}
+hipError_t launch_gemm_ws_(const RowGemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return hipSuccess;
   if (g.K != WS_K || g.N % 512 || g.N <= 0 || (g.epi == RE_RES_LN && g.N != 512) ||
       g.fault.kind != FK_NONE || (g.epi == RE_RELU_QUANT_PMAX && g.pmax_n <= 0))
