@@ -70,7 +70,7 @@ def head_max(ctx):
     return np.abs(ctx).reshape(-1, 8, 64).max(-1).T
 
 
-@pytest.mark.parametrize("M", [1, 2, 16, 32, 45])
+@pytest.mark.parametrize("M", [1, 2, 16, 32, 45, 100, 256])
 @pytest.mark.parametrize("N,K,flags,bits", [(512, 512, 2, 8), (1536, 512, 0, 8),
                                              (2048, 512, 5, 8), (512, 2048, 2, 4)])
 def test_skinny_i8(torch, M, N, K, flags, bits):
@@ -91,7 +91,7 @@ def test_skinny_i8(torch, M, N, K, flags, bits):
         np.testing.assert_array_equal(pm.cpu().numpy(), tile_max(y))
 
 
-@pytest.mark.parametrize("M", [2, 5, 32])
+@pytest.mark.parametrize("M", [2, 5, 32, 98, 256])
 def test_skinny_layernorm_prologue(torch, M, oracle_model):
     rng = np.random.default_rng(M)
     x = (rng.standard_normal((M, 512)) * 3).astype(f32)
@@ -108,14 +108,15 @@ def test_skinny_layernorm_prologue(torch, M, oracle_model):
     np.testing.assert_array_equal(pm.cpu().numpy(), tile_max(y))
 
 
-@pytest.mark.parametrize("M", [1, 3, 5, 32, 40])
+@pytest.mark.parametrize("M", [1, 3, 5, 32, 40, 100, 200, 256])
 @pytest.mark.parametrize("K,nparts", [(2048, 128), (2048, 32), (512, 8), (512, 1)])
 def test_skinny_partial_max_prologue(torch, M, K, nparts):
     """amode 2: fp32 rows quantized per token from partial row maxima (FFN2 from FFN1's
     per-tile maxima — 128 of 16 columns or 32 of 64 (k_skinny_wide); the output projection
     from the attention's per-head maxima).  K = 2048 with 8-bit weights and the residual
     runs the 8-wave k_skinny8_ffn2 up to M = 32 (M not a multiple of its 4-row blocks: 1, 3,
-    5), the 4-wave k_skinny above (40)."""
+    5), the 4-wave k_skinny above (40) with 8- / 16-row blocks from M = 96 / 192 (100, 200,
+    256), where the K = 512 projection runs N-split (k_skinny_wide, 8-row blocks)."""
     rng = np.random.default_rng(M + K + nparts)
     h = np.maximum(rng.standard_normal((M, K)), 0).astype(f32)
     h[0] = 0                                         # an all-zero row: clamp 1e-5
