@@ -1262,7 +1262,10 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
                       int64_t* ids, const uint8_t* src_mask, hipStream_t st) {
   const qtx_config& c = m->cfg;
   const int D = c.d_model, F = c.d_ff, wb = m->dec[0].qkv.q8 ? 8 : c.weight_bits;
-  const bool ffn_qkernel = knobs().ffn_qkernel;
+  // the FFN hidden quantized once by its own kernel (instead of in every FFN2 workgroup's
+  // prologue from FFN1's partial maxima) from 96 rows on: measured faster there despite the
+  // extra launch (profiles/r05_rb_sweep.md), slower at B = 32
+  const bool ffn_qkernel = knobs().ffn_qkernel || B >= 96;
   const bool fused_ln = !knobs().split_ln;
   Scratch& s = g.dec;
   // Timing experiments only (wrong results): QTX_ABLATE=<bitmask> drops kernel classes

@@ -506,9 +506,10 @@ hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
   // =<rb>: every K = 512 launch (experiments).
   // From M >= 96 (the decode of >= 96 sentences per sub-batch, e.g. cfg5's 256 per GPU) the
   // small blocks re-read W once per 4 rows: there every K = 512 GEMM runs N-split with 8-row
-  // blocks and FFN2's fp32-prologue K-split with 8 (M < 192) or 16-row blocks
-  // (tools/rb_sweep256.py, profiles/r05_rb_sweep.md: B = 256 decode 35.0 -> 29.0 ms,
-  // B = 128 23.1 -> 21.7 ms; at B = 32 / 64 the small blocks stay faster).
+  // blocks, and FFN2 (whose hidden the decode step then quantizes with its own kernel,
+  // qtx_api.hip greedy_step_fused) takes 16-row blocks — or 8 / 16 with the fp32 prologue
+  // (tools/rb_sweep256.py, profiles/r05_rb_sweep.md: B = 256 decode 35.0 -> 27.5 ms,
+  // B = 128 23.1 -> 21.0 ms; at B = 32 / 64 the small blocks stay faster).
   const Knobs& kn = knobs();     // QTX_SKINNY_WIDE / QTX_RB_* / QTX_SKINNY8_MAXM: QTX_DIAG build
   const bool big = g.M >= 96;
   const int wide_env = kn.skinny_wide;
@@ -533,7 +534,7 @@ hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
       k_skinny8_ffn2<<<dim3(g.N / 16, (g.M + 3) / 4), 512, 0, st>>>(g);
       return hipGetLastError();
     }
-    const int rb_i8 = kn.rb_i8_2048;
+    const int rb_i8 = kn.rb_i8_2048 > 0 ? kn.rb_i8_2048 : (big ? 16 : 4);
     const int rb_f = kn.rb_f32q > 0 ? kn.rb_f32q : (g.M >= 192 ? 16 : big ? 8 : 4);
     if (g.amode == A_I8) return skinny_rb<2048, WB, A_I8>(g, rb_i8, st);
     if (g.amode == A_F32Q) return skinny_rb<2048, WB, A_F32Q>(g, rb_f, st);

@@ -58,8 +58,8 @@ struct Knobs {
   bool wsp_pmax_sr5 = false; // QTX_WSP_PMAX_SR5
   bool wsa2 = false;         // QTX_WSA2
   int skinny_wide = -1;      // QTX_SKINNY_WIDE
-  int rb_i8_512 = 4, rb_ln = 4, rb_i8_2048 = 4;   // QTX_RB_*
-  int rb_f32q = 0;           // QTX_RB_F32Q (0: by M, qtx_decode.hip skinny_mode)
+  int rb_i8_512 = 4, rb_ln = 4;   // QTX_RB_*
+  int rb_i8_2048 = 0, rb_f32q = 0;  // QTX_RB_I8_2048 / _F32Q (0: by M, qtx_decode.hip skinny_mode)
   int skinny8_maxm = 32;     // QTX_SKINNY8_MAXM
   int ws32 = 0;              // QTX_WS32: Q/K/V + FFN1 on k_gemm_wsq32 / wsy32 (32x32x32 MFMA;
                              // 2: Q/K/V with all of W in registers)

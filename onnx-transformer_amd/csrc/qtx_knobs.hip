@@ -63,7 +63,7 @@ Knobs read_env() {
   k.skinny_wide = (int)num("QTX_SKINNY_WIDE", -1);
   k.rb_i8_512 = (int)num("QTX_RB_I8_512", 4);
   k.rb_ln = (int)num("QTX_RB_LN", 4);
-  k.rb_i8_2048 = (int)num("QTX_RB_I8_2048", 4);
+  k.rb_i8_2048 = (int)num("QTX_RB_I8_2048", 0);
   k.rb_f32q = (int)num("QTX_RB_F32Q", 0);
   k.skinny8_maxm = (int)num("QTX_SKINNY8_MAXM", 32);
   k.ws32 = (int)num("QTX_WS32", 0);

@@ -72,7 +72,8 @@ def head_max(ctx):
 
 @pytest.mark.parametrize("M", [1, 2, 16, 32, 45, 100, 256])
 @pytest.mark.parametrize("N,K,flags,bits", [(512, 512, 2, 8), (1536, 512, 0, 8),
-                                             (2048, 512, 5, 8), (512, 2048, 2, 4)])
+                                             (2048, 512, 5, 8), (512, 2048, 2, 4),
+                                             (512, 2048, 2, 8)])
 def test_skinny_i8(torch, M, N, K, flags, bits):
     rng = np.random.default_rng(M + N + K + flags)
     qx, sx = O.quant_rows(rng.standard_normal((M, K)).astype(f32))

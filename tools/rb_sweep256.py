@@ -18,7 +18,8 @@ from qtx import _lib  # noqa: E402
 from qtx.model import QtxModel  # noqa: E402
 from qtx.weights import ModelConfig, synthetic_state_dict  # noqa: E402
 
-KNOBS = ("QTX_RB_I8_512", "QTX_RB_LN", "QTX_RB_I8_2048", "QTX_RB_F32Q", "QTX_SKINNY_WIDE")
+KNOBS = ("QTX_RB_I8_512", "QTX_RB_LN", "QTX_RB_I8_2048", "QTX_RB_F32Q", "QTX_SKINNY_WIDE",
+         "QTX_FFN_QKERNEL", "QTX_SPLIT_LN")
 CONFIGS = [
     {},
     {"QTX_SKINNY_WIDE": "8"},
@@ -29,6 +30,17 @@ CONFIGS = [
     {"QTX_SKINNY_WIDE": "4", "QTX_RB_F32Q": "16"},
     {"QTX_SKINNY_WIDE": "16", "QTX_RB_F32Q": "16"},
 ]
+if os.environ.get("RB_SWEEP_SET") == "3":   # the hidden / LayerNorm done once per row
+    CONFIGS = [
+        {},
+        {"QTX_FFN_QKERNEL": "1"},
+        {"QTX_FFN_QKERNEL": "1", "QTX_RB_I8_2048": "16"},
+        {"QTX_FFN_QKERNEL": "1", "QTX_RB_I8_2048": "32"},
+        {"QTX_SPLIT_LN": "1"},
+        {"QTX_SPLIT_LN": "1", "QTX_FFN_QKERNEL": "1", "QTX_RB_I8_2048": "16"},
+        {"QTX_RB_F32Q": "32"},
+        {"QTX_RB_F32Q": "8"},
+    ]
 if os.environ.get("RB_SWEEP_SET") == "1":   # the first sweep's single-knob set
     CONFIGS = [
         {},
