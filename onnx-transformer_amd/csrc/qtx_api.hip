@@ -1261,7 +1261,8 @@ SkinnyArgs skinny(int wbits, const QLin& L, int M, int amode, int flags, float* 
 int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len,
                       int64_t* ids, const uint8_t* src_mask, hipStream_t st) {
   const qtx_config& c = m->cfg;
-  const int D = c.d_model, F = c.d_ff, wb = m->dec[0].qkv.q8 ? 8 : c.weight_bits;
+  const int D = c.d_model, F = c.d_ff;
+  const int wb = m->dec[0].qkv.q8 && !knobs().int4_packed ? 8 : c.weight_bits;
   // the FFN hidden quantized once by its own kernel (instead of in every FFN2 workgroup's
   // prologue from FFN1's partial maxima) from 96 rows on: measured faster there despite the
   // extra launch (profiles/r05_rb_sweep.md), slower at B = 32
