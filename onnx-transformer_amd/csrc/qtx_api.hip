@@ -1258,8 +1258,10 @@ SkinnyArgs skinny(int wbits, const QLin& L, int M, int amode, int flags, float* 
 //   [LN+QKV] [self-attn] [O+res] [LN+Qc] [cross-attn] [Oc+res] [LN+FFN1+relu] [FFN2+res]
 //   [final LN + generator] [log_softmax/argmax + next embedding + step++]
 // Reads the position from g.step (device), so it can be captured once and replayed.
+// t_host: the step's position when the caller knows it at launch or capture time (the
+// whole decode in one graph, or eager launches), else -1
 int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len,
-                      int64_t* ids, const uint8_t* src_mask, hipStream_t st) {
+                      int64_t* ids, const uint8_t* src_mask, hipStream_t st, int t_host) {
   const qtx_config& c = m->cfg;
   const int D = c.d_model, F = c.d_ff;
   const int wb = m->dec[0].qkv.q8 && !knobs().int4_packed ? 8 : c.weight_bits;
@@ -1315,6 +1317,7 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
     at.y = s.y; at.ldy = 3 * D; at.kv_new = 1; at.step = g.step;
     at.kc = g.kc[l]; at.vc = g.vc[l]; at.skc = g.skc[l]; at.svc = g.svc[l]; at.kv_bs = max_len;
     at.ctx = s.ctx; at.pmax = g.pmax_a; at.B = B;
+    at.host_step1 = t_host >= 0 && !knobs().device_step ? t_host + 1 : 0;
     QTX_RUN(4, launch_dec_attn(at, B, st));
     a = skinny(wb, L.o, B, A_F32Q, EPI_RESIDUAL, s.x, D);   // quantizes ctx per token
     a.X = s.ctx; a.ldx = D; a.pmax_in = g.pmax_a; a.pmax_n = 8; a.res = s.x; a.ldr = D;
@@ -1676,9 +1679,9 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
     HIPCHK(launch_embed(ids + (long)gr.b0(i) * max_len, max_len, gr.rows(i, B), 1, gv[i].step,
                         0, m->tgt_lut, c.tgt_vocab, m->pe, c.max_len, gv[i].dec.x, D, st));
   }
-  auto step_fn = [&](int i, hipStream_t s) {
+  auto step_fn = [&](int i, hipStream_t s, int t) {
     return greedy_step_fused(m, gv[i], gr.rows(i, B), S, max_len, ids + (long)gr.b0(i) * max_len,
-                             src_mask + (long)gr.b0(i) * S, s);
+                             src_mask + (long)gr.b0(i) * S, s, t);
   };
   // One decode step per sub-batch captured once per (shape, buffers) as a hipGraph on its
   // own stream and replayed max_len-1 times there; the streams fork from and join back
@@ -1699,7 +1702,7 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
       for (int i = 0; i < gr.G; ++i) HIPCHK(hipStreamWaitEvent(mm->gstream[i], mm->ev_in, 0));
     }
     for (int t = 0; t + 1 < max_len; ++t)
-      for (int i = 0; i < gr.G; ++i) RC(step_fn(i, fk ? mm->gstream[i] : st));
+      for (int i = 0; i < gr.G; ++i) RC(step_fn(i, fk ? mm->gstream[i] : st, t));
     if (fk)
       for (int i = 0; i < gr.G; ++i) {
         HIPCHK(hipEventRecord(mm->ev_out[i], mm->gstream[i]));
@@ -1712,13 +1715,17 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
   int per_graph = max_len - 1;
   if (const int v = knobs().graph_steps; v > 0 && (max_len - 1) % v == 0) per_graph = v;
   if (max_len <= 1) return QTX_OK;
+  // a graph of the whole decode is replayed once per decode from position 0: each captured
+  // step knows its position (a shorter graph replays at several)
+  const bool known = per_graph == max_len - 1;
   const bool joint = gr.G > 1 && knobs().group_graph;
   // the switches a captured step depends on are part of its key (knobs can be reloaded)
   const Knobs& kn = knobs();
   // (every switch: the key carries the knob generation, bumped by each reload — ADVICE r04:
   // QTX_SKINNY_WIDE, QTX_RB_*, ... pick launch shapes inside the captured step too)
   const std::string variant = std::to_string(knobs_generation()) + ":" + std::to_string(kn.split_ln) +
-                              std::to_string(kn.ffn_qkernel) + std::to_string(kn.group_graph);
+                              std::to_string(kn.ffn_qkernel) + std::to_string(kn.group_graph) +
+                              std::to_string(kn.device_step);
   const GraphKey key{B, S, max_len, gr.G * 1000 + per_graph, g.gsteps, variant};
   auto it = mm->graphs.find(key);
   if (it == mm->graphs.end()) {
@@ -1737,7 +1744,7 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
       hipError_t e = hipEventRecord(mm->ev_in, s0);
       for (int i = 1; i < gr.G && e == hipSuccess; ++i) e = hipStreamWaitEvent(mm->gstream[i], mm->ev_in, 0);
       for (int t = 0; t < per_graph && rc == QTX_OK && e == hipSuccess; ++t)
-        for (int i = 0; i < gr.G && rc == QTX_OK; ++i) rc = step_fn(i, mm->gstream[i]);
+        for (int i = 0; i < gr.G && rc == QTX_OK; ++i) rc = step_fn(i, mm->gstream[i], known ? t : -1);
       for (int i = 1; i < gr.G && e == hipSuccess; ++i) {
         e = hipEventRecord(mm->ev_out[i], mm->gstream[i]);
         if (e == hipSuccess) e = hipStreamWaitEvent(s0, mm->ev_out[i], 0);
@@ -1759,7 +1766,7 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
       hipError_t e = hipStreamBeginCapture(mm->gstream[i], hipStreamCaptureModeThreadLocal);
       if (e != hipSuccess) { drop(); HIPCHK(e); }
       int rc = QTX_OK;
-      for (int t = 0; t < per_graph && rc == QTX_OK; ++t) rc = step_fn(i, mm->gstream[i]);
+      for (int t = 0; t < per_graph && rc == QTX_OK; ++t) rc = step_fn(i, mm->gstream[i], known ? t : -1);
       e = hipStreamEndCapture(mm->gstream[i], &graph);
       if (rc != QTX_OK || e != hipSuccess) {
         if (graph) (void)hipGraphDestroy(graph);

@@ -571,7 +571,8 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   const int b = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
   QTX_STAMP(0);
   const float* yr = a.y + (long)b * a.ldy;
-  const int nrows = KV_NEW ? (int)a.kv_bs : a.S;   // rows staged (self: all allocated rows)
+  // rows staged (self: rows 0 .. the position when the host passes it, else all allocated)
+  const int nrows = KV_NEW ? (a.host_step1 > 0 ? a.host_step1 : (int)a.kv_bs) : a.S;
   const long kvb = (long)b * a.kv_bs;
 
   // phase 0: every global load first (one memory latency): this step's q (k, v) rows
@@ -591,7 +592,7 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   const float k_own = KV_NEW ? yr[512 + h * 64 + lane] : 0.0f;
   const float v_own = KV_NEW ? yr[1024 + h * 64 + lane] : 0.0f;
   // clamped: a stale position (a counter not reset) must not index past the cache
-  const int step = KV_NEW ? min(max(*a.step, 0), (int)a.kv_bs - 1) : 0;
+  const int step = !KV_NEW ? 0 : a.host_step1 > 0 ? a.host_step1 - 1 : min(max(*a.step, 0), (int)a.kv_bs - 1);
   const int rsub = lane >> 2, ch = lane & 3;
   uint4 kr[NIT], vr[NIT];
 #pragma unroll
@@ -749,8 +750,9 @@ hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st) {
   if (B <= 0) return hipSuccess;
   if (!a.ctx || !a.pmax || a.B != B) return hipErrorInvalidValue;
   if (a.kv_new) {
-    if (a.kv_bs <= 0 || a.kv_bs > DEC_MAXK) return hipErrorInvalidValue;
-    return dec_attn_nit<true>(a, B, (int)a.kv_bs, st);
+    if (a.kv_bs <= 0 || a.kv_bs > DEC_MAXK || a.host_step1 < 0 || a.host_step1 > a.kv_bs)
+      return hipErrorInvalidValue;
+    return dec_attn_nit<true>(a, B, a.host_step1 > 0 ? a.host_step1 : (int)a.kv_bs, st);
   }
   if (a.S <= 0 || a.S > DEC_MAXK) return hipErrorInvalidValue;
   return dec_attn_nit<false>(a, B, a.S, st);

@@ -63,6 +63,10 @@ struct DecAttnArgs {
   const uint8_t* mask;        // cross: [B, S]
   float* ctx; float* pmax;    // out
   int B, kv_new;
+  // self: the position + 1 when the host knows it (a decode step captured at its own
+  // position): no read of *step, and only rows 0 .. position staged; 0: read *step and stage
+  // all kv_bs rows (a step replayed at several positions)
+  int host_step1;
 };
 
 // Row quantizer / LayerNorm+quantizer over rows of D floats (one wave per row).
