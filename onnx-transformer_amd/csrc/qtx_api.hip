@@ -1270,6 +1270,9 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
   // extra launch (profiles/r05_rb_sweep.md), slower at B = 32
   const bool ffn_qkernel = knobs().ffn_qkernel || B >= 96;
   const bool fused_ln = !knobs().split_ln;
+  // O / Oc form the context's per-token maximum from the rows they load (A_F32R) instead of
+  // the attention's per-head maxima (QTX_ATTN_PMAX=1: the per-head maxima, A_F32Q)
+  const bool own_max = !knobs().attn_pmax;
   Scratch& s = g.dec;
   // Timing experiments only (wrong results): QTX_ABLATE=<bitmask> drops kernel classes
   // from the step (replaced by an empty kernel with QTX_ABLATE_NOP=1) to measure what
@@ -1316,10 +1319,10 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
     DecAttnArgs at{};
     at.y = s.y; at.ldy = 3 * D; at.kv_new = 1; at.step = g.step;
     at.kc = g.kc[l]; at.vc = g.vc[l]; at.skc = g.skc[l]; at.svc = g.svc[l]; at.kv_bs = max_len;
-    at.ctx = s.ctx; at.pmax = g.pmax_a; at.B = B;
+    at.ctx = s.ctx; at.pmax = own_max ? nullptr : g.pmax_a; at.B = B;
     at.host_step1 = t_host >= 0 && !knobs().device_step ? t_host + 1 : 0;
     QTX_RUN(4, launch_dec_attn(at, B, st));
-    a = skinny(wb, L.o, B, A_F32Q, EPI_RESIDUAL, s.x, D);   // quantizes ctx per token
+    a = skinny(wb, L.o, B, own_max ? A_F32R : A_F32Q, EPI_RESIDUAL, s.x, D);   // quantizes ctx per token
     a.X = s.ctx; a.ldx = D; a.pmax_in = g.pmax_a; a.pmax_n = 8; a.res = s.x; a.ldr = D;
     QTX_RUN(16, launch_skinny(a, wb, st));
     RC(ln_linear(L.cq, L.ln[1], 0, s.y, D, 2));
@@ -1327,9 +1330,9 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
     at.y = s.y; at.ldy = D; at.kv_new = 0; at.S = S; at.mask = src_mask;
     at.kc = g.cross.k8[l]; at.vc = g.cross.v8[l]; at.skc = g.cross.sk[l];
     at.svc = g.cross.sv[l]; at.kv_bs = S;
-    at.ctx = s.ctx; at.pmax = g.pmax_a; at.B = B;
+    at.ctx = s.ctx; at.pmax = own_max ? nullptr : g.pmax_a; at.B = B;
     QTX_RUN(8, launch_dec_attn(at, B, st));
-    a = skinny(wb, L.co, B, A_F32Q, EPI_RESIDUAL, s.x, D);
+    a = skinny(wb, L.co, B, own_max ? A_F32R : A_F32Q, EPI_RESIDUAL, s.x, D);
     a.X = s.ctx; a.ldx = D; a.pmax_in = g.pmax_a; a.pmax_n = 8; a.res = s.x; a.ldr = D;
     QTX_RUN(16, launch_skinny(a, wb, st));
     if (!ffn_qkernel) {   // FFN2 quantizes h itself from FFN1's per-tile row maxima
@@ -1947,8 +1950,8 @@ int32_t qtx_skinny_linear(int32_t amode, const int8_t* A, const float* sa, const
                           float* pmax_out, void* stream) {
   if (!W || !sw || !bias || !out) return fail(QTX_E_INVALID, "null argument");
   if ((amode == A_I8 && (!A || !sa)) || (amode == A_LN && (!X || !ln_a || !ln_b)) ||
-      (amode == A_F32Q && (!X || !pmax_in || pmax_n <= 0 || pmax_n > 128)) || amode < 0 ||
-      amode > 2)
+      (amode == A_F32Q && (!X || !pmax_in || pmax_n <= 0 || pmax_n > 128)) ||
+      (amode == A_F32R && (!X || K != 512)) || amode < 0 || amode > 3)
     return fail(QTX_E_INVALID, "operands missing for amode %d", amode);
   if (((flags & EPI_RESIDUAL) && !res) || ((flags & EPI_ROWMAX) && !pmax_out))
     return fail(QTX_E_INVALID, "flags need res / pmax_out");

@@ -108,6 +108,8 @@ __device__ __forceinline__ void skinny_prologue(const SkinnyArgs& g, uint8_t* As
       if (lane == 0) sas[r] = ok ? sc[j] : 0.0f;
     }
   } else {  // A_F32Q: each wave's rows (<= 4 at a time) with their partial maxima
+            // A_F32R: the same rows, the row maximum from the row itself
+    constexpr bool OWN = AMODE == A_F32R;
     constexpr int NC = K / 256, RBT = RPW < 4 ? RPW : 4;
 #pragma unroll
     for (int j0 = 0; j0 < RPW; j0 += RBT) {
@@ -119,16 +121,27 @@ __device__ __forceinline__ void skinny_prologue(const SkinnyArgs& g, uint8_t* As
 #pragma unroll
         for (int c = 0; c < NC; ++c)
           t[jb][c] = *reinterpret_cast<const float4*>(g.X + (long)m * g.ldx + 4 * (lane + 64 * c));
+        if constexpr (!OWN)
 #pragma unroll
-        for (int u = 0; u < 2; ++u)   // lane takes partials lane, lane+64 (clamped: max-safe)
-          pm[jb][u] = g.pmax_in[(long)min(lane + 64 * u, g.pmax_n - 1) * g.M + m];
+          for (int u = 0; u < 2; ++u)   // lane takes partials lane, lane+64 (clamped: max-safe)
+            pm[jb][u] = g.pmax_in[(long)min(lane + 64 * u, g.pmax_n - 1) * g.M + m];
       }
       if (j0 == 0) issue_rest();
 #pragma unroll
       for (int jb = 0; jb < RBT; ++jb) {
         const int r = wave + 4 * (j0 + jb);
         const bool ok = m0 + r < g.M;
-        const float sc = quant_scale(wave_max(fmaxf(pm[jb][0], pm[jb][1])), 127.0f);
+        float lm;
+        if constexpr (OWN) {   // |x| max of this lane's values (fmaxf: NaN drops out as in
+          lm = 0.0f;           // the partial maxima the producer would have formed)
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+            lm = fmaxf(lm, fmaxf(fmaxf(fabsf(t[jb][c].x), fabsf(t[jb][c].y)),
+                                 fmaxf(fabsf(t[jb][c].z), fabsf(t[jb][c].w))));
+        } else {
+          lm = fmaxf(pm[jb][0], pm[jb][1]);
+        }
+        const float sc = quant_scale(wave_max(lm), 127.0f);
         uint32_t* dst = reinterpret_cast<uint32_t*>(As + r * LDA);
         float tf[4 * NC];
 #pragma unroll
@@ -519,12 +532,14 @@ hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
     if (g.amode == A_I8) return skinny_wide_rb<WB, A_I8>(g, rb, st);
     if (g.amode == A_LN) return skinny_wide_rb<WB, A_LN>(g, rb, st);
     if (g.amode == A_F32Q) return skinny_wide_rb<WB, A_F32Q>(g, rb, st);
+    if (g.amode == A_F32R) return skinny_wide_rb<WB, A_F32R>(g, rb, st);
   }
   if (g.K == 512) {
     const int rb_i8 = kn.rb_i8_512, rb_ln = kn.rb_ln;
     if (g.amode == A_I8) return skinny_rb<512, WB, A_I8>(g, g.M <= 4 ? 4 : rb_i8, st);
     if (g.amode == A_LN) return skinny_rb<512, WB, A_LN>(g, rb_ln, st);
     if (g.amode == A_F32Q) return skinny_rb<512, WB, A_F32Q>(g, g.M <= 4 ? 4 : rb_i8, st);
+    if (g.amode == A_F32R) return skinny_rb<512, WB, A_F32R>(g, g.M <= 4 ? 4 : rb_i8, st);
   } else if (g.K == 2048) {
     // the decode FFN2 (fp32 hidden, residual, 8-bit weights) at M <= QTX_SKINNY8_MAXM
     // (default 32): 8 waves (measured: B = 32 decode 14.45 -> 14.40 ms; at B = 256 the
@@ -721,11 +736,14 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
     acc = fmaf(P[j], (float)(int8_t)Vs[j * 64 + lane] * svs[j], acc);
   QTX_STAMP(3);
 
-  // phase 5: this head's 64 context values and their absmax; the consumer GEMM takes the
-  // row maximum over the 8 heads and quantizes the row per token (A_F32Q prologue)
+  // phase 5: this head's 64 context values (and their absmax when asked for: the consumer
+  // GEMM then takes the row maximum over the 8 heads, A_F32Q; the fused decode's consumer
+  // forms it from the row itself, A_F32R)
   a.ctx[(long)b * 512 + h * 64 + lane] = acc;
-  const float am = wave_max(fabsf(acc));
-  if (lane == 0) a.pmax[(long)h * a.B + b] = am;
+  if (a.pmax) {
+    const float am = wave_max(fabsf(acc));
+    if (lane == 0) a.pmax[(long)h * a.B + b] = am;
+  }
   QTX_STAMP(4);
 }
 
@@ -748,7 +766,7 @@ hipError_t dec_attn_nit(const DecAttnArgs& a, int B, int nrows, hipStream_t st) 
 
 hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st) {
   if (B <= 0) return hipSuccess;
-  if (!a.ctx || !a.pmax || a.B != B) return hipErrorInvalidValue;
+  if (!a.ctx || a.B != B) return hipErrorInvalidValue;
   if (a.kv_new) {
     if (a.kv_bs <= 0 || a.kv_bs > DEC_MAXK || a.host_step1 < 0 || a.host_step1 > a.kv_bs)
       return hipErrorInvalidValue;

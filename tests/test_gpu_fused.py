@@ -133,6 +133,25 @@ def test_skinny_partial_max_prologue(torch, M, K, nparts):
                                   res + O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b))
 
 
+@pytest.mark.parametrize("M", [1, 3, 5, 32, 40, 100, 256])
+def test_skinny_own_max_prologue(torch, M):
+    """amode 3: fp32 rows [M, 512] quantized per token from their own row absmax (the fused
+    decode's O / Oc projections: the context rows the GEMM loads anyway), the same results
+    as amode 2 over complete partial maxima."""
+    rng = np.random.default_rng(M + 3)
+    h = rng.standard_normal((M, 512)).astype(f32)
+    h[0] = 0                                         # an all-zero row: clamp 1e-5
+    qw, sw, b = weights(rng, 512, 512, 8)
+    res = rng.standard_normal((M, 512)).astype(f32)
+    out = dev(torch, res.copy())
+    call("qtx_skinny_linear", 3, S0, S0, P(dev(torch, h)), 512, S0, S0, S0, 0,
+         P(dev(torch, qw)), P(dev(torch, sw)), P(dev(torch, b)), M, 512, 512, 8, 2,
+         P(out), P(out), S0, S0)
+    qx, sx = O.quant_rows(h)
+    np.testing.assert_array_equal(out.cpu().numpy(),
+                                  res + O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b))
+
+
 @pytest.mark.parametrize("B,step,kv_bs", [(2, 0, 8), (3, 5, 8), (32, 40, 72), (1, 127, 128),
                                           (4, 70, 72), (2, 15, 17)])
 def test_decode_self_attention(torch, B, step, kv_bs):
