@@ -333,10 +333,10 @@ int32_t qtx_pack_w_ws(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* 
  * in the prologue: amode 0 = int8 A [M,K] + sa; 1 = LayerNorm(X [M,512]; ln_a, ln_b) then
  * per-token quant; 2 = fp32 X [M,K] quantized per token with s = max(m, 1e-5)/127 where m =
  * max over p < pmax_n of pmax_in[p*M + row] (partial row absmaxima, e.g. per head or per
- * column tile; pmax_n <= 128); 3 = fp32 X [M,512] quantized per token from its own row
+ * column tile; pmax_n <= 128); 3 = fp32 X [M,K] quantized per token from its own row
  * absmax (the scale amode 2 forms from complete partials).  flags: 1 ReLU, 2 residual
  * (res), 4 partial row absmax of the output per 16-column tile into pmax_out [N/16][M].
- * N % 16 == 0, K in {512, 2048} (amodes 1, 3: K = 512).  quant_linear.py:111-119,
+ * N % 16 == 0, K in {512, 2048} (amode 1: K = 512).  quant_linear.py:111-119,
  * layer_norm.py:12-15. */
 int32_t qtx_skinny_linear(int32_t amode, const int8_t* A, const float* sa, const float* X,
                           int64_t ldx, const float* ln_a, const float* ln_b,

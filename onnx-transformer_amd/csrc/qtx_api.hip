@@ -1273,6 +1273,9 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
   // O / Oc form the context's per-token maximum from the rows they load (A_F32R) instead of
   // the attention's per-head maxima (QTX_ATTN_PMAX=1: the per-head maxima, A_F32Q)
   const bool own_max = !knobs().attn_pmax;
+  // likewise FFN2 forms the hidden's per-token maximum itself (QTX_FFN_PMAX=1: from FFN1's
+  // per-tile maxima, FFN1 with the maxima epilogue)
+  const bool ffn_own = !knobs().ffn_pmax;
   Scratch& s = g.dec;
   // Timing experiments only (wrong results): QTX_ABLATE=<bitmask> drops kernel classes
   // from the step (replaced by an empty kernel with QTX_ABLATE_NOP=1) to measure what
@@ -1335,9 +1338,9 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
     a = skinny(wb, L.co, B, own_max ? A_F32R : A_F32Q, EPI_RESIDUAL, s.x, D);
     a.X = s.ctx; a.ldx = D; a.pmax_in = g.pmax_a; a.pmax_n = 8; a.res = s.x; a.ldr = D;
     QTX_RUN(16, launch_skinny(a, wb, st));
-    if (!ffn_qkernel) {   // FFN2 quantizes h itself from FFN1's per-tile row maxima
-      RC(ln_linear(L.w1, L.ln[2], EPI_RELU | EPI_ROWMAX, s.y, F, 32));
-      a = skinny(wb, L.w2, B, A_F32Q, EPI_RESIDUAL, s.x, D);
+    if (!ffn_qkernel) {   // FFN2 quantizes h itself (from its rows, or FFN1's per-tile maxima)
+      RC(ln_linear(L.w1, L.ln[2], ffn_own ? EPI_RELU : EPI_RELU | EPI_ROWMAX, s.y, F, 32));
+      a = skinny(wb, L.w2, B, ffn_own ? A_F32R : A_F32Q, EPI_RESIDUAL, s.x, D);
       a.X = s.y; a.ldx = F; a.pmax_in = g.pmax_f; a.pmax_n = F / 16; a.res = s.x; a.ldr = D;
       QTX_RUN(128, launch_skinny(a, wb, st));
     } else {              // one wave per row quantizes h (quant_linear.py:30-43), then FFN2
@@ -1951,7 +1954,7 @@ int32_t qtx_skinny_linear(int32_t amode, const int8_t* A, const float* sa, const
   if (!W || !sw || !bias || !out) return fail(QTX_E_INVALID, "null argument");
   if ((amode == A_I8 && (!A || !sa)) || (amode == A_LN && (!X || !ln_a || !ln_b)) ||
       (amode == A_F32Q && (!X || !pmax_in || pmax_n <= 0 || pmax_n > 128)) ||
-      (amode == A_F32R && (!X || K != 512)) || amode < 0 || amode > 3)
+      (amode == A_F32R && !X) || amode < 0 || amode > 3)
     return fail(QTX_E_INVALID, "operands missing for amode %d", amode);
   if (((flags & EPI_RESIDUAL) && !res) || ((flags & EPI_ROWMAX) && !pmax_out))
     return fail(QTX_E_INVALID, "flags need res / pmax_out");

@@ -293,12 +293,16 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
 // (16 values per lane: half the dependent quantization chain of k_skinny's one row per
 // wave), K split 8 ways (4 weight fragments per lane), exact int32 reduction over the 8
 // waves.  Rows per workgroup 4, 16 columns.  Bit-identical to k_skinny.
+// OWN (A_F32R): the row maximum from the row itself — each wave's half-row maximum, the two
+// halves met through LDS — instead of FFN1's per-tile partial maxima.
 // =====================================================================================
+template <bool OWN>
 __global__ __launch_bounds__(512) void k_skinny8_ffn2(SkinnyArgs g) {
   constexpr int K = 2048, RB = 4, KW = K / 8, NS = KW / 64, LDA = K + 16;
   __shared__ __attribute__((aligned(16))) uint8_t As[16 * LDA];
   __shared__ float sas[16];
   __shared__ v4i red[7][64];
+  __shared__ float hmax[8];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * RB;
@@ -309,9 +313,10 @@ __global__ __launch_bounds__(512) void k_skinny8_ffn2(SkinnyArgs g) {
 #pragma unroll
   for (int c = 0; c < 4; ++c)
     t[c] = *reinterpret_cast<const float4*>(g.X + (long)m * g.ldx + 4 * (lane + 64 * (4 * half + c)));
-  float pm[2];
+  float pm[2] = {0.0f, 0.0f};
+  if constexpr (!OWN)
 #pragma unroll
-  for (int u = 0; u < 2; ++u) pm[u] = g.pmax_in[(long)min(lane + 64 * u, g.pmax_n - 1) * g.M + m];
+    for (int u = 0; u < 2; ++u) pm[u] = g.pmax_in[(long)min(lane + 64 * u, g.pmax_n - 1) * g.M + m];
   // 2. then this wave's weight fragments and (wave 0) the epilogue operands
   const int n = min(n0 + fr, g.N - 1);
   uint4 wf[NS];
@@ -327,7 +332,20 @@ __global__ __launch_bounds__(512) void k_skinny8_ffn2(SkinnyArgs g) {
   // 3. per-token quantization of the half row into LDS
   {
     const bool ok = m0 + r < g.M;
-    const float sc = quant_scale(wave_max(fmaxf(pm[0], pm[1])), 127.0f);
+    float rmax;
+    if constexpr (OWN) {
+      float lm = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        lm = fmaxf(lm, fmaxf(fmaxf(fabsf(t[c].x), fabsf(t[c].y)), fmaxf(fabsf(t[c].z), fabsf(t[c].w))));
+      lm = wave_max(lm);
+      if (lane == 0) hmax[wave] = lm;
+      __syncthreads();
+      rmax = fmaxf(hmax[2 * r], hmax[2 * r + 1]);
+    } else {
+      rmax = wave_max(fmaxf(pm[0], pm[1]));
+    }
+    const float sc = quant_scale(rmax, 127.0f);
     float tf[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -545,14 +563,19 @@ hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
     // (default 32): 8 waves (measured: B = 32 decode 14.45 -> 14.40 ms; at B = 256 the
     // 4-wave kernel is faster, 35.1 vs 36.8 ms)
     const int sk8_maxm = kn.skinny8_maxm;
-    if (g.M <= sk8_maxm && WB == 8 && g.amode == A_F32Q && g.flags == EPI_RESIDUAL && g.pmax_n <= 128) {
-      k_skinny8_ffn2<<<dim3(g.N / 16, (g.M + 3) / 4), 512, 0, st>>>(g);
+    if (g.M <= sk8_maxm && WB == 8 && g.flags == EPI_RESIDUAL &&
+        ((g.amode == A_F32Q && g.pmax_n <= 128) || g.amode == A_F32R)) {
+      if (g.amode == A_F32R)
+        k_skinny8_ffn2<true><<<dim3(g.N / 16, (g.M + 3) / 4), 512, 0, st>>>(g);
+      else
+        k_skinny8_ffn2<false><<<dim3(g.N / 16, (g.M + 3) / 4), 512, 0, st>>>(g);
       return hipGetLastError();
     }
     const int rb_i8 = kn.rb_i8_2048 > 0 ? kn.rb_i8_2048 : (big ? 16 : 4);
     const int rb_f = kn.rb_f32q > 0 ? kn.rb_f32q : (g.M >= 192 ? 16 : big ? 8 : 4);
     if (g.amode == A_I8) return skinny_rb<2048, WB, A_I8>(g, rb_i8, st);
     if (g.amode == A_F32Q) return skinny_rb<2048, WB, A_F32Q>(g, rb_f, st);
+    if (g.amode == A_F32R) return skinny_rb<2048, WB, A_F32R>(g, rb_f, st);
   }
   return hipErrorInvalidValue;
 }

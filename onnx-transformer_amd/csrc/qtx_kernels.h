@@ -32,7 +32,7 @@ enum : int {
   A_I8 = 0,    // int8 A [M,K] + sa[M]
   A_LN = 1,    // fp32 X [M,512]: LayerNorm(ln_a, ln_b) + per-token quant in the prologue
   A_F32Q = 2,  // fp32 X [M,K] + partial absmax: quant with s = max(max_p pmax,1e-5)/127
-  A_F32R = 3,  // fp32 X [M,512] quantized per token from its own row absmax (no partials)
+  A_F32R = 3,  // fp32 X [M,K] quantized per token from its own row absmax (no partials)
 };
 enum : int {
   EPI_ROWMAX = 4,  // pmax_out[tile][m] = max |y| over the tile's 16 columns (last)

@@ -134,18 +134,22 @@ def test_skinny_partial_max_prologue(torch, M, K, nparts):
 
 
 @pytest.mark.parametrize("M", [1, 3, 5, 32, 40, 100, 256])
-def test_skinny_own_max_prologue(torch, M):
-    """amode 3: fp32 rows [M, 512] quantized per token from their own row absmax (the fused
-    decode's O / Oc projections: the context rows the GEMM loads anyway), the same results
-    as amode 2 over complete partial maxima."""
-    rng = np.random.default_rng(M + 3)
-    h = rng.standard_normal((M, 512)).astype(f32)
+@pytest.mark.parametrize("K", [512, 2048])
+def test_skinny_own_max_prologue(torch, M, K):
+    """amode 3: fp32 rows [M, K] quantized per token from their own row absmax (the fused
+    decode's O / Oc projections and FFN2: rows the GEMM loads anyway; K = 2048 up to M = 32
+    runs k_skinny8_ffn2, whose two half-row waves meet their maxima in LDS), the same
+    results as amode 2 over complete partial maxima."""
+    rng = np.random.default_rng(M + K + 3)
+    h = rng.standard_normal((M, K)).astype(f32)
+    if K == 2048:
+        h = np.maximum(h, 0)                         # a ReLU hidden
     h[0] = 0                                         # an all-zero row: clamp 1e-5
-    qw, sw, b = weights(rng, 512, 512, 8)
+    qw, sw, b = weights(rng, 512, K, 8)
     res = rng.standard_normal((M, 512)).astype(f32)
     out = dev(torch, res.copy())
-    call("qtx_skinny_linear", 3, S0, S0, P(dev(torch, h)), 512, S0, S0, S0, 0,
-         P(dev(torch, qw)), P(dev(torch, sw)), P(dev(torch, b)), M, 512, 512, 8, 2,
+    call("qtx_skinny_linear", 3, S0, S0, P(dev(torch, h)), K, S0, S0, S0, 0,
+         P(dev(torch, qw)), P(dev(torch, sw)), P(dev(torch, b)), M, 512, K, 8, 2,
          P(out), P(out), S0, S0)
     qx, sx = O.quant_rows(h)
     np.testing.assert_array_equal(out.cpu().numpy(),
