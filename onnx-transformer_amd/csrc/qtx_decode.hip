@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
   constexpr int LDA = K + 16;     // padded LDS row (bytes)
   __shared__ __attribute__((aligned(16))) uint8_t As[BM * LDA];
   __shared__ float sas[BM];
-  __shared__ v4i red[3][MF][64];
+  __shared__ v4i red[4][MF][64];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
   uint2 wp[NS];
   const int col = n0 + fr;
   const bool cok = col < g.N;
-  float swc = 0.0f, bc = 0.0f, rv[MF][4];
+  float swc = 0.0f, bc = 0.0f, rv[MF];
   constexpr bool resid = FLAGS & EPI_RESIDUAL;
   auto issue_rest = [&]() {
 #pragma unroll
@@ -210,14 +210,12 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
     const int cc = min(col, g.N - 1);
     swc = g.sw[cc];
     bc = g.bias[cc];
-    if constexpr (resid) {
+    if constexpr (resid) {   // the rows this wave finishes: 4 fg + wave of each tile
 #pragma unroll
-      for (int i = 0; i < MF; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = min(m0 + 16 * i + 4 * fg + e, g.M - 1);
-          rv[i][e] = g.res[(long)row * g.ldr + cc];
-        }
+      for (int i = 0; i < MF; ++i) {
+        const int row = min(m0 + 16 * i + 4 * fg + wave, g.M - 1);
+        rv[i] = g.res[(long)row * g.ldr + cc];
+      }
     }
   };
 
@@ -251,28 +249,26 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
   }
 
   // 4. exact int32 reduction of the 4 K ranges
-  if (wave > 0)
 #pragma unroll
-    for (int i = 0; i < MF; ++i) red[wave - 1][i][lane] = acc[i];
+  for (int i = 0; i < MF; ++i) red[wave][i][lane] = acc[i];
   __syncthreads();
-  if (wave != 0) return;
   QTX_STAMP(2);
-#pragma unroll
-  for (int w = 0; w < 3; ++w)
-#pragma unroll
-    for (int i = 0; i < MF; ++i) acc[i] += red[w][i][lane];
-
-  // 5. epilogue (C layout: col = lane & 15, row = 4*(lane>>4) + e)
+  // 5. epilogue, split over the waves: wave w finishes element e = w of every lane's four
+  //    (C layout: col = lane & 15, row = 4*(lane>>4) + e), its int32 sum over the 4 K ranges
+  //    exact in any order
   constexpr bool relu = FLAGS & EPI_RELU, rmax = FLAGS & EPI_ROWMAX;
+  const int e = wave;
 #pragma unroll
   for (int i = 0; i < MF; ++i) {
+    {
+      int sum = 0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+      for (int w = 0; w < 4; ++w) sum += reinterpret_cast<const int*>(&red[w][i][lane])[e];
       const int r = 16 * i + 4 * fg + e, row = m0 + r;
       const bool ok = cok && r < RB && row < g.M;
-      float y = ((float)acc[i][e] * sas[r]) * swc + bc;
+      float y = ((float)sum * sas[r]) * swc + bc;
       if constexpr (relu) y = y > 0.0f ? y : 0.0f;
-      if constexpr (resid) y = rv[i][e] + y;
+      if constexpr (resid) y = rv[i] + y;
       if (ok) g.out[(long)row * g.ldo + col] = y;
       if constexpr (rmax) {
         float am = ok ? fabsf(y) : 0.0f;   // max over the 16 lanes (columns) of this row
