@@ -297,7 +297,7 @@ __global__ __launch_bounds__(512) void k_skinny8_ffn2(SkinnyArgs g) {
   constexpr int K = 2048, RB = 4, KW = K / 8, NS = KW / 64, LDA = K + 16;
   __shared__ __attribute__((aligned(16))) uint8_t As[16 * LDA];
   __shared__ float sas[16];
-  __shared__ v4i red[7][64];
+  __shared__ v4i red[8][64];
   __shared__ float hmax[8];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
@@ -322,9 +322,8 @@ __global__ __launch_bounds__(512) void k_skinny8_ffn2(SkinnyArgs g) {
   const int col = n0 + fr, cc = min(col, g.N - 1);
   const bool cok = col < g.N;
   const float swc = g.sw[cc], bc = g.bias[cc];
-  float rv[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) rv[e] = g.res[(long)min(m0 + 4 * fg + e, g.M - 1) * g.ldr + cc];
+  // the epilogue's output of this lane (wave 0): row m0 + (lane >> 4), column n0 + (lane & 15)
+  const float rv = g.res[(long)min(m0 + fg, g.M - 1) * g.ldr + cc];
   // 3. per-token quantization of the half row into LDS
   {
     const bool ok = m0 + r < g.M;
@@ -362,17 +361,21 @@ __global__ __launch_bounds__(512) void k_skinny8_ffn2(SkinnyArgs g) {
     const v4i afr = *reinterpret_cast<const v4i*>(As + fr * LDA + wave * KW + 64 * s + 16 * fg);
     acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr, __builtin_bit_cast(v4i, wf[s]), acc, 0, 0, 0);
   }
-  if (wave > 0) red[wave - 1][lane] = acc;
+  red[wave][lane] = acc;
   __syncthreads();
   if (wave != 0) return;
+  // 5. epilogue: out = res + y.  The RB = 4 useful rows of the 16-row tile sit in lanes
+  //    0-15 (element e = row); wave 0 takes one output per lane — lane l: row e = l >> 4,
+  //    column l & 15 — summing element e of lane l & 15 over the 8 K ranges (exact int32;
+  //    conflict-free LDS reads)
+  {
+    const int e = fg, src = fr;
+    int sum = 0;
 #pragma unroll
-  for (int w = 0; w < 7; ++w) acc += red[w][lane];
-  // 5. epilogue: out = res + y (rows 4fg + e < RB of the 16-row MFMA tile)
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int rr = 4 * fg + e, row = m0 + rr;
-    const float y = ((float)acc[e] * sas[rr]) * swc + bc;
-    if (cok && rr < RB && row < g.M) g.out[(long)row * g.ldo + col] = rv[e] + y;
+    for (int w = 0; w < 8; ++w) sum += reinterpret_cast<const int*>(&red[w][src])[e];
+    const int row = m0 + e;
+    const float y = ((float)sum * sas[e]) * swc + bc;
+    if (cok && row < g.M) g.out[(long)row * g.ldo + col] = rv + y;
   }
 }
 
