@@ -393,6 +393,7 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
   static_assert(RB % 4 == 0 && RB <= 16, "rows per block");
   __shared__ __attribute__((aligned(16))) uint8_t As[16 * LDA];
   __shared__ float sas[16];
+  __shared__ v4i tail[RB == 4 ? 4 : 1][16];   // RB = 4: each wave's useful C rows, remapped
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
   const int n0 = blockIdx.x * 64 + 16 * wave, m0 = blockIdx.y * RB;
@@ -421,10 +422,14 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
     }
     swc = cok ? g.sw[col] : 0.0f;
     bc = cok ? g.bias[col] : 0.0f;
+    if constexpr (RB == 4) {   // the epilogue's one output per lane: row m0 + fg
+      rv[0] = (resid && cok && m0 + fg < g.M) ? g.res[(long)(m0 + fg) * g.ldr + col] : 0.0f;
+    } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int r = 4 * fg + e, row = m0 + r;
-      rv[e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * fg + e, row = m0 + r;
+        rv[e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
+      }
     }
   };
   // 2. A panel and per-row scales into LDS
@@ -448,6 +453,29 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
   QTX_STAMP(2);
   // 4. epilogue (C layout: col = lane & 15, row = 4*(lane>>4) + e)
   constexpr bool relu = FLAGS & EPI_RELU, rmax = FLAGS & EPI_ROWMAX;
+  if constexpr (RB == 4) {
+    // the 4 useful rows are elements 0-3 of lanes 0-15: through the wave's own LDS slot
+    // (in-order within the wave, conflict-free) lane l takes row l >> 4 of column l & 15 —
+    // one output per lane instead of four on a quarter of the lanes
+    if (fg == 0) tail[wave][fr] = acc;
+    const int v = reinterpret_cast<const int*>(&tail[wave][fr])[fg];
+    const int row = m0 + fg;
+    const bool ok = cok && row < g.M;
+    float y = ((float)v * sas[fg]) * swc + bc;
+    if constexpr (relu) y = y > 0.0f ? y : 0.0f;
+    if constexpr (resid) y = rv[0] + y;
+    if (ok) g.out[(long)row * g.ldo + col] = y;
+    if constexpr (rmax) {
+      float am = ok ? fabsf(y) : 0.0f;   // max over the 16 lanes (columns) of this row
+      am = fmaxf(am, dpp<0xB1>(am));
+      am = fmaxf(am, dpp<0x4E>(am));
+      am = fmaxf(am, dpp<0x141>(am));
+      am = fmaxf(am, dpp<0x140>(am));
+      if (fr == 0 && row < g.M) g.pmax_out[(long)(n0 >> 4) * g.M + row] = am;
+    }
+    QTX_STAMP(3);
+    return;
+  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int r = 4 * fg + e, row = m0 + r;
