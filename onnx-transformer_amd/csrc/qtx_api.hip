@@ -1276,6 +1276,10 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
   // likewise FFN2 forms the hidden's per-token maximum itself (QTX_FFN_PMAX=1: from FFN1's
   // per-tile maxima, FFN1 with the maxima epilogue)
   const bool ffn_own = !knobs().ffn_pmax;
+  // the position from the host (self-attention, argmax + embedding; the device counter then
+  // neither read nor advanced) or from the device counter (QTX_DEVICE_STEP, or a step replayed
+  // at several positions)
+  const bool host_pos = t_host >= 0 && !knobs().device_step;
   Scratch& s = g.dec;
   // Timing experiments only (wrong results): QTX_ABLATE=<bitmask> drops kernel classes
   // from the step (replaced by an empty kernel with QTX_ABLATE_NOP=1) to measure what
@@ -1323,7 +1327,7 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
     at.y = s.y; at.ldy = 3 * D; at.kv_new = 1; at.step = g.step;
     at.kc = g.kc[l]; at.vc = g.vc[l]; at.skc = g.skc[l]; at.svc = g.svc[l]; at.kv_bs = max_len;
     at.ctx = s.ctx; at.pmax = own_max ? nullptr : g.pmax_a; at.B = B;
-    at.host_step1 = t_host >= 0 && !knobs().device_step ? t_host + 1 : 0;
+    at.host_step1 = host_pos ? t_host + 1 : 0;
     QTX_RUN(4, launch_dec_attn(at, B, st));
     a = skinny(wb, L.o, B, own_max ? A_F32R : A_F32Q, EPI_RESIDUAL, s.x, D);   // quantizes ctx per token
     a.X = s.ctx; a.ldx = D; a.pmax_in = g.pmax_a; a.pmax_n = 8; a.res = s.x; a.ldr = D;
@@ -1365,7 +1369,7 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
                                      m->gen_b, c.tgt_vocab, g.logits, st));
   QTX_RUN(256, launch_argmax_embed(g.logits, B, c.tgt_vocab, ids, max_len, g.step,
                                    reinterpret_cast<unsigned*>(g.step + 1), m->tgt_lut, m->pe,
-                                   c.max_len, s.x, st));
+                                   c.max_len, s.x, st, host_pos ? t_host + 1 : 0));
   return QTX_OK;
 #undef QTX_RUN
 #undef QTX_RUNRC

@@ -994,16 +994,19 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
          (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
 }
 
+// host_s1: the position + 1 when the host knows it (then no read of *step and no step
+// advance: nothing of a decode whose every step knows its position reads the counter);
+// 0: read *step and advance it (the last workgroup to arrive)
 __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int V, int64_t* ids,
                                                        long ids_bs, int* step, unsigned* arrive,
                                                        const float* lut, const float* pe,
-                                                       int max_pos, float* xnext) {
+                                                       int max_pos, float* xnext, int host_s1) {
   __shared__ float Ev[ARG_MAXV];
   __shared__ float redf[16], lse_s;
   __shared__ int redi[16], redc[16], redb[16];
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   QTX_STAMP(0);
-  const int s = *step;
+  const int s = host_s1 > 0 ? host_s1 - 1 : *step;
   const float* x = logits + (long)m * V;
   float4 pe_row = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // position s+1 is known up front
   if (tid < 128) pe_row = *reinterpret_cast<const float4*>(pe + (long)min(s + 1, max_pos - 1) * 512 + 4 * tid);
@@ -1100,7 +1103,7 @@ __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int 
   }
   QTX_STAMP(5);
   // every workgroup has read *step above; the last one to arrive advances it
-  if (tid == 0) {
+  if (host_s1 == 0 && tid == 0) {
     const unsigned tk = atomicAdd(arrive, 1u);
     if (tk == gridDim.x - 1) {
       *step = s + 1;
@@ -1111,11 +1114,11 @@ __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int 
 
 hipError_t launch_argmax_embed(const float* logits, int M, int V, int64_t* ids, long ids_bs,
                                int* step, unsigned* arrive, const float* lut, const float* pe,
-                               int max_pos, float* xnext, hipStream_t st) {
+                               int max_pos, float* xnext, hipStream_t st, int host_s1) {
   if (M <= 0) return hipSuccess;
-  if (V > ARG_MAXV) return hipErrorInvalidValue;
+  if (V > ARG_MAXV || host_s1 < 0) return hipErrorInvalidValue;
   k_argmax_embed<<<dim3(M), dim3(ARG_T), 0, st>>>(logits, V, ids, ids_bs, step, arrive, lut,
-                                                  pe, max_pos, xnext);
+                                                  pe, max_pos, xnext, host_s1);
   return hipGetLastError();
 }
 

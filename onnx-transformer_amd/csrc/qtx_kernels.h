@@ -223,7 +223,7 @@ hipError_t launch_pack_gen(const float* W, int V, float* out, hipStream_t st);
 //   the last workgroup to finish advances *step (arrive is its private counter).
 hipError_t launch_argmax_embed(const float* logits, int M, int V, int64_t* ids, long ids_bs,
                                int* step, unsigned* arrive, const float* lut, const float* pe,
-                               int max_pos, float* xnext, hipStream_t st);
+                               int max_pos, float* xnext, hipStream_t st, int host_s1 = 0);
 hipError_t launch_rows(const RowArgs& a, hipStream_t st);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st);
 hipError_t launch_embed(const int64_t* ids, long ids_bs, int B, int T, const int* pos_dev,
