@@ -19,7 +19,7 @@ from qtx.model import QtxModel  # noqa: E402
 from qtx.weights import ModelConfig, synthetic_state_dict  # noqa: E402
 
 KNOBS = ("QTX_RB_I8_512", "QTX_RB_LN", "QTX_RB_I8_2048", "QTX_RB_F32Q", "QTX_SKINNY_WIDE",
-         "QTX_FFN_QKERNEL", "QTX_SPLIT_LN", "QTX_ATTN_PM")
+         "QTX_FFN_QKERNEL", "QTX_SPLIT_LN", "QTX_ATTN_PM", "QTX_DEC_ATTN_GRP")
 CONFIGS = [
     {},
     {"QTX_SKINNY_WIDE": "8"},
@@ -30,6 +30,8 @@ CONFIGS = [
     {"QTX_SKINNY_WIDE": "4", "QTX_RB_F32Q": "16"},
     {"QTX_SKINNY_WIDE": "16", "QTX_RB_F32Q": "16"},
 ]
+if os.environ.get("RB_SWEEP_SET") == "5":   # decode attention: one workgroup per sentence
+    CONFIGS = [{}, {"QTX_DEC_ATTN_GRP": "0"}, {"QTX_DEC_ATTN_GRP": "1"}]
 if os.environ.get("RB_SWEEP_SET") == "4":   # attention scales from partial maxima
     CONFIGS = [{}, {"QTX_ATTN_PM": "0"}, {"QTX_ATTN_PM": "1"}]
 if os.environ.get("RB_SWEEP_SET") == "3":   # the hidden / LayerNorm done once per row
