@@ -30,6 +30,8 @@ CONFIGS = [
     {"QTX_SKINNY_WIDE": "4", "QTX_RB_F32Q": "16"},
     {"QTX_SKINNY_WIDE": "16", "QTX_RB_F32Q": "16"},
 ]
+if os.environ.get("RB_SWEEP_SET") == "6":   # every K = 512 GEMM N-split at small batches
+    CONFIGS = [{}, {"QTX_SKINNY_WIDE": "4"}, {"QTX_SKINNY_WIDE": "8"}]
 if os.environ.get("RB_SWEEP_SET") == "5":   # decode attention: one workgroup per sentence
     CONFIGS = [{}, {"QTX_DEC_ATTN_GRP": "0"}, {"QTX_DEC_ATTN_GRP": "1"}]
 if os.environ.get("RB_SWEEP_SET") == "4":   # attention scales from partial maxima
