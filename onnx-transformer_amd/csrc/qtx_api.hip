@@ -1349,7 +1349,10 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
       QTX_RUN(128, launch_skinny(a, wb, st));
     } else {              // one wave per row quantizes h (quant_linear.py:30-43), then FFN2
       RC(ln_linear(L.w1, L.ln[2], EPI_RELU, s.y, F, 32));
-      QTX_RUNRC(64, quant(s.y, F, B, F, s.a8, s.sa, st));
+      if (F == 2048 && !knobs().hquant_rows)   // one 4-wave workgroup per row
+        QTX_RUN(64, launch_quant_h2048(s.y, F, B, s.a8, s.sa, st));
+      else
+        QTX_RUNRC(64, quant(s.y, F, B, F, s.a8, s.sa, st));
       a = skinny(wb, L.w2, B, A_I8, EPI_RESIDUAL, s.x, D);
       a.A = s.a8; a.sa = s.sa; a.res = s.x; a.ldr = D;
       QTX_RUN(128, launch_skinny(a, wb, st));

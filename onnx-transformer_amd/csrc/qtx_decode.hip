@@ -827,6 +827,48 @@ hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st) {
 }
 
 // =====================================================================================
+// k_quant_h2048: per-token quantization of fp32 rows of 2048 (the decode FFN's hidden from
+// B >= 96, quant_linear.py:30-43): one 4-wave workgroup per row, wave w quarter w (8 values
+// per lane), the row maximum met in LDS — a quarter of k_rows' one-wave-per-row chain.  The
+// same scale (quant_scale of the row absmax, order-free) and codes (quant_pack).
+// =====================================================================================
+__global__ __launch_bounds__(256) void k_quant_h2048(const float* X, long ldx, int M,
+                                                     int8_t* q, float* s) {
+  __shared__ float wm[4];
+  const int m = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const float* xr = X + (long)m * ldx + 512 * wave;
+  float4 t[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) t[c] = *reinterpret_cast<const float4*>(xr + 4 * (lane + 64 * c));
+  float lm = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+    lm = fmaxf(lm, fmaxf(fmaxf(fabsf(t[c].x), fabsf(t[c].y)), fmaxf(fabsf(t[c].z), fabsf(t[c].w))));
+  lm = wave_max(lm);
+  if (lane == 0) wm[wave] = lm;
+  __syncthreads();
+  const float sc = quant_scale(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])), 127.0f);
+  float tf[8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    tf[4 * c] = t[c].x; tf[4 * c + 1] = t[c].y; tf[4 * c + 2] = t[c].z; tf[4 * c + 3] = t[c].w;
+  }
+  uint32_t qd[2];
+  quant_pack<8>(tf, sc, qd);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(q + (long)m * 2048 + 512 * wave);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) dst[lane + 64 * c] = qd[c];
+  if (tid == 0) s[m] = sc;
+}
+
+hipError_t launch_quant_h2048(const float* X, long ldx, int M, int8_t* q, float* s,
+                              hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  k_quant_h2048<<<dim3(M), dim3(256), 0, st>>>(X, ldx, M, q, s);
+  return hipGetLastError();
+}
+
+// =====================================================================================
 // k_generator_mfma: the canonical generator order on the fp32 matrix cores.
 // logits[m, v] = ((c0 + c1) + (c2 + c3)) + b[v] with c_q the k-ordered fma chain over
 // k in [128q, 128q + 128) from 0 (oracle OracleModel.logits): v_mfma_f32_16x16x4_f32 chained

@@ -211,6 +211,9 @@ hipError_t launch_pack_ffn(const int8_t* W1, const int8_t* W2, int F, int8_t* ou
 hipError_t launch_gemm(const GemmArgs& a, int wbits, hipStream_t st);
 hipError_t launch_skinny(const SkinnyArgs& a, int wbits, hipStream_t st);
 hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st);
+// per-token int8 quantization of fp32 rows of 2048 (q row-major [M, 2048], s [M])
+hipError_t launch_quant_h2048(const float* X, long ldx, int M, int8_t* q, float* s,
+                              hipStream_t st);
 // generator with the final LayerNorm fused in (ln_a may be null = no LN)
 // the same on fp32 MFMA (bit-identical chain); Wt = generator weight transposed [512][V]
 hipError_t launch_generator_mfma(const float* x, long ldx, int M, const float* ln_a,

@@ -30,6 +30,7 @@ struct Knobs {
   bool wsr_off = false;      // QTX_WSR=0: the O-projection's WS epilogue on k_gemm_ws
   bool attn_pmax = false;    // QTX_ATTN_PMAX: the decode O / Oc from the attention's per-head maxima
   bool ffn_pmax = false;     // QTX_FFN_PMAX: the decode FFN2 from FFN1's per-tile maxima
+  bool hquant_rows = false;  // QTX_HQUANT_ROWS: the decode hidden quantized by k_rows
   bool device_step = false;  // QTX_DEVICE_STEP: self-attention reads its position from the
                              // device counter even where the host knows it
   bool int4_packed = false;  // QTX_INT4_PACKED: a 4-bit model's decode step on the packed int4 kernels

@@ -38,6 +38,7 @@ Knobs read_env() {
   k.wsr_off = getenv("QTX_WSR") && *getenv("QTX_WSR") == '0';
   k.attn_pmax = flag("QTX_ATTN_PMAX");
   k.ffn_pmax = flag("QTX_FFN_PMAX");
+  k.hquant_rows = flag("QTX_HQUANT_ROWS");
   k.device_step = flag("QTX_DEVICE_STEP");
   k.int4_packed = flag("QTX_INT4_PACKED");
   k.decode_groups = (int)num("QTX_DECODE_GROUPS", 0);

@@ -70,7 +70,7 @@ def test_greedy_decode_matches_oracle(torch, gpu_model, oracle_model, golden_mod
                                  {"QTX_DECODE_GROUPS": "2", "QTX_GROUP_GRAPH": "1"},
                                  {"QTX_SPLIT_LN": "1"}, {"QTX_FFN_QKERNEL": "1"},
                                  {"QTX_DEVICE_STEP": "1"}, {"QTX_ATTN_PMAX": "1"},
-                                 {"QTX_FFN_PMAX": "1"}])
+                                 {"QTX_FFN_PMAX": "1"}, {"QTX_HQUANT_ROWS": "1"}])
 def test_greedy_paths_agree(torch, gpu_model, knob_env, env):
     """The fused+graph decode step, the fused eager step, the unfused kernels, graphs of
     several steps and sub-batches on several streams agree."""

@@ -19,7 +19,8 @@ from qtx.model import QtxModel  # noqa: E402
 from qtx.weights import ModelConfig, synthetic_state_dict  # noqa: E402
 
 KNOBS = ("QTX_RB_I8_512", "QTX_RB_LN", "QTX_RB_I8_2048", "QTX_RB_F32Q", "QTX_SKINNY_WIDE",
-         "QTX_FFN_QKERNEL", "QTX_SPLIT_LN", "QTX_ATTN_PM", "QTX_DEC_ATTN_GRP")
+         "QTX_FFN_QKERNEL", "QTX_SPLIT_LN", "QTX_ATTN_PM", "QTX_DEC_ATTN_GRP",
+         "QTX_HQUANT_ROWS")
 CONFIGS = [
     {},
     {"QTX_SKINNY_WIDE": "8"},
@@ -30,6 +31,8 @@ CONFIGS = [
     {"QTX_SKINNY_WIDE": "4", "QTX_RB_F32Q": "16"},
     {"QTX_SKINNY_WIDE": "16", "QTX_RB_F32Q": "16"},
 ]
+if os.environ.get("RB_SWEEP_SET") == "7":   # the hidden's quantization kernel
+    CONFIGS = [{}, {"QTX_HQUANT_ROWS": "1"}]
 if os.environ.get("RB_SWEEP_SET") == "6":   # every K = 512 GEMM N-split at small batches
     CONFIGS = [{}, {"QTX_SKINNY_WIDE": "4"}, {"QTX_SKINNY_WIDE": "8"}]
 if os.environ.get("RB_SWEEP_SET") == "5":   # decode attention: one workgroup per sentence
