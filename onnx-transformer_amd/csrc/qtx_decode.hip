@@ -393,7 +393,10 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
   static_assert(RB % 4 == 0 && RB <= 16, "rows per block");
   __shared__ __attribute__((aligned(16))) uint8_t As[16 * LDA];
   __shared__ float sas[16];
-  __shared__ v4i tail[RB == 4 ? 4 : 1][16];   // RB = 4: each wave's useful C rows, remapped
+  // RB = 4 / 8: each wave's useful C rows (lanes 0 .. 4 RB - 1), remapped through LDS
+  constexpr int RPL = RB / 4;                        // outputs per lane after the remap
+  constexpr bool REMAP = RB == 4 || RB == 8;
+  __shared__ v4i tail[REMAP ? 4 : 1][REMAP ? 4 * RB : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
   const int n0 = blockIdx.x * 64 + 16 * wave, m0 = blockIdx.y * RB;
@@ -424,6 +427,12 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
     bc = cok ? g.bias[col] : 0.0f;
     if constexpr (RB == 4) {   // the epilogue's one output per lane: row m0 + fg
       rv[0] = (resid && cok && m0 + fg < g.M) ? g.res[(long)(m0 + fg) * g.ldr + col] : 0.0f;
+    } else if constexpr (RB == 8) {   // its two: rows m0 + fg, m0 + fg + 4
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = m0 + fg + 4 * j;
+        rv[j] = (resid && cok && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
+      }
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -472,6 +481,32 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
       am = fmaxf(am, dpp<0x141>(am));
       am = fmaxf(am, dpp<0x140>(am));
       if (fr == 0 && row < g.M) g.pmax_out[(long)(n0 >> 4) * g.M + row] = am;
+    }
+    QTX_STAMP(3);
+    return;
+  }
+  if constexpr (RB == 8) {
+    // the 8 useful rows are elements 0-3 of lanes 0-31 (row 4 (l >> 4) + e): the same
+    // remap, lane l takes rows (l >> 4) and (l >> 4) + 4 of column l & 15 — two outputs per
+    // lane instead of four on half of the lanes
+    if (fg < RPL) tail[wave][16 * fg + fr] = acc;
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int v = reinterpret_cast<const int*>(&tail[wave][16 * j + fr])[fg];
+      const int r = fg + 4 * j, row = m0 + r;
+      const bool ok = cok && row < g.M;
+      float y = ((float)v * sas[r]) * swc + bc;
+      if constexpr (relu) y = y > 0.0f ? y : 0.0f;
+      if constexpr (resid) y = rv[j] + y;
+      if (ok) g.out[(long)row * g.ldo + col] = y;
+      if constexpr (rmax) {
+        float am = ok ? fabsf(y) : 0.0f;   // max over the 16 lanes (columns) of this row
+        am = fmaxf(am, dpp<0xB1>(am));
+        am = fmaxf(am, dpp<0x4E>(am));
+        am = fmaxf(am, dpp<0x141>(am));
+        am = fmaxf(am, dpp<0x140>(am));
+        if (fr == 0 && row < g.M) g.pmax_out[(long)(n0 >> 4) * g.M + row] = am;
+      }
     }
     QTX_STAMP(3);
     return;
