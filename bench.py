@@ -206,23 +206,32 @@ def pmc_traffic():
 
 
 def profiler_dominant(B, alg):
-    """The dominant kernel's average per-dispatch duration at the decode grid in the newest
-    committed rocprofv3 kernel stats of this bench (tools/prof_summary.py "by launch grid"
-    table), with the roofline fraction it implies — the profiler's view next to the live
-    HIP-event figure, or None when no profile lists the kernel at that grid."""
+    """A labelled side field, not the headline: the dominant kernel's average per-dispatch
+    duration at the decode grid in the newest committed rocprofv3 kernel stats of this bench
+    (tools/prof_summary.py "by launch grid" table) and the fraction it implies, with whether
+    that profile was taken from the kernel sources this run is built from (its
+    kernel_sources_sha16 line against tools/prof_summary.py's digest of csrc/ now), or None
+    when no profile lists the kernel at that grid."""
     import glob
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from prof_summary import sources_sha16
     grid = f"{(D // 16) * 256}x{(B + 3) // 4}"          # 16 columns x 4 rows per workgroup
     for fn in sorted(glob.glob(os.path.join(REPO, "profiles", "*_bench_kernel_stats.md")), reverse=True):
+        sha = None
         with open(fn) as f:
             for line in f:
+                if line.startswith("kernel_sources_sha16:"):
+                    sha = line.split(":", 1)[1].strip()
                 cells = [c.strip() for c in line.split("|")]
                 if len(cells) > 6 and DOMINANT in cells[1] and cells[2].startswith(grid + " "):
                     us = float(cells[5])
                     return {"source": os.path.relpath(fn, REPO), "avg_us": us,
                             "achieved": alg / (us * 1e-6) / 1e9, "frac": alg / (us * 1e-6) / PEAK_HBM,
+                            "profiled_sources_sha16": sha,
+                            "matches_current_sources": sha == sources_sha16() if sha else None,
                             "note": "rocprofv3 per-dispatch durations of the graph-replayed "
-                                    "decode kernels; the profiler serializes graph dispatches, "
-                                    "so they read longer than the live per-node time"}
+                                    "decode kernels; the profiler dispatches graph nodes one at "
+                                    "a time, so they read longer than the live per-node time"}
     return None
 
 
@@ -541,25 +550,23 @@ def main():
         # durations of graph-replayed nodes are inflated by the profiler (an empty kernel
         # reads 4.6 us there, 1.6 us per node live: profiles/r03b_dominant_timing.md)
         alg = dominant_alg_bytes(Bd)
-        # achieved / frac follow from the committed rocprofv3 summary of this bench (VERDICT
-        # r04: per-dispatch durations, profiles/*_bench_kernel_stats.md); the live chain
-        # timing sits beside it (the profiler serializes graph nodes, so its per-dispatch
-        # times read longer than the live per-node time the decode sees)
+        # achieved / frac from THIS run's measurement: the live chain, us per
+        # node with its launch boundary included (conservative); the committed rocprofv3
+        # per-dispatch view is a labelled side field ("profiler"), flagged when it was taken
+        # from other kernel sources than the ones this run is built from
         prof = profiler_dominant(Bd, alg)
-        kt = (prof["avg_us"] if prof else chain_us) * 1e-6
+        kt = chain_us * 1e-6
         roof = {"kernel": f"{DOMINANT}: decode O / Oc projection (M={Bd}, N={D}, K={D}, int8, "
                           "fp32 context quantized per token in the prologue, residual epilogue)",
                 "bound": "hbm", "achieved": alg / kt / 1e9, "peak": PEAK_HBM / 1e9,
                 "unit": "GB/s", "frac": alg / kt / PEAK_HBM, "traffic": pmc_traffic(),
-                "avg_us": kt * 1e6, "alg_bytes_per_launch": alg,
-                "source": prof["source"] if prof else "live chain (no committed kernel stats)",
-                "live": {"avg_us": chain_us, "achieved": alg / (chain_us * 1e-6) / 1e9,
-                         "frac": alg / (chain_us * 1e-6) / PEAK_HBM, "empty_node_us": nop_us,
-                         "marginal_us": chain_us - nop_us,
-                         "method": f"hipGraph chain of 256 dependent launches over "
-                                   f"{DOMINANT_COPIES} rotating operand sets, HIP events on the "
-                                   "replay stream: us per node (launch boundary included); "
-                                   "empty_node_us = the same chain of empty kernels"}}
+                "avg_us": chain_us, "alg_bytes_per_launch": alg,
+                "empty_node_us": nop_us, "marginal_us": chain_us - nop_us,
+                "method": f"live, this run: hipGraph chain of 256 dependent launches over "
+                          f"{DOMINANT_COPIES} rotating operand sets at the decode grid, HIP "
+                          "events on the replay stream: us per node (launch boundary "
+                          "included); empty_node_us = the same chain of empty kernels",
+                "profiler": prof}
         # the whole decode step: (decode of max_len - 1 steps) - (decode of 1 step), per step
         t_full = time_decode(model, Bd, S, L)
         t_one = time_decode(model, Bd, S, 2)

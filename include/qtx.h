@@ -220,11 +220,13 @@ int32_t qtx_pack_int4(const int8_t* q, int32_t N, int32_t K, uint8_t* packed, vo
 
 /* Attention core on quantized Q/K/V laid out [B,S,H*64] with per-token scales [B,S]:
  * ctx [B,Sq,H*64] fp32.  mask uint8 [B,Sq,Sk] with strides (m_bs, m_is) in elements
- * (m_is = 0 broadcasts one row, e.g. the encoder's [B,1,S] mask); NULL = keep all. */
+ * (m_is = 0 broadcasts one row, e.g. the encoder's [B,1,S] mask); NULL = keep all.
+ * dec != 0: a decoder layer's attention (decoder.py:28-33), whose PV MatMul runs in the
+ * decoder's canonical order (four partial chains); 0: the encoder's. */
 int32_t qtx_attention_i8(const int8_t* q, const float* sq, const int8_t* k, const float* sk,
                          const int8_t* v, const float* sv, const uint8_t* mask, int64_t m_bs,
                          int64_t m_is, int32_t B, int32_t H, int32_t Sq, int32_t Sk,
-                         float* ctx, void* stream);
+                         float* ctx, int32_t dec, void* stream);
 
 /* qtx_attention_i8 plus the attention MatMuls' intermediates, for the traced executor
  * (run_module(expose_intermediates=...), onnx_optimized_inference.py:57 stores every node
@@ -235,7 +237,7 @@ int32_t qtx_attention_i8(const int8_t* q, const float* sq, const int8_t* k, cons
 int32_t qtx_attention_trace(const int8_t* q, const float* sq, const int8_t* k, const float* sk,
                             const int8_t* v, const float* sv, const uint8_t* mask, int64_t m_bs,
                             int64_t m_is, int32_t B, int32_t H, int32_t Sq, int32_t Sk,
-                            float* ctx, float* qk_acc, float* p_codes, void* stream);
+                            float* ctx, float* qk_acc, float* p_codes, int32_t dec, void* stream);
 
 /* Encoder self-attention with the context quantized per token for the O-projection
  * (attention.py:23-67 + quant_linear.py:30-43, replacing the MatMul_{8L+3,8L+4} pair of the
@@ -352,7 +354,8 @@ int32_t qtx_skinny_linear(int32_t amode, const int8_t* A, const float* sa, const
  * kv_new = 0 (cross): y [B,512] holds q; keys = S cached rows per sentence, mask [B,S].
  * Caches: kc/vc int8 [B][kv_bs][512], skc/svc [B][kv_bs].  Out: fp32 context ctx [B,512]
  * and the per-head absmax pmax [8][B] (the next GEMM's per-token quantization, amode 2 of
- * qtx_skinny_linear with pmax_n = 8).  Keys <= 128. */
+ * qtx_skinny_linear with pmax_n = 8).  Keys <= 128.  The PV MatMul runs in the decoder's
+ * canonical order (four partial chains; qtx_attention_i8 with dec = 1). */
 int32_t qtx_decode_attention(int32_t kv_new, const float* y, int64_t ldy, int8_t* kc,
                              int8_t* vc, float* skc, float* svc, int32_t kv_bs,
                              const int32_t* step_dev, int32_t S, const uint8_t* mask,

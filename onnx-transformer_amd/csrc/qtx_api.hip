@@ -799,7 +799,7 @@ AttnArgs attn_args(const Scratch& s, int B, int Sq, int Sk, long kbs_rows) {
 // attention.py:39-67).  Q/K/V come out of ONE N=3D GEMM and are quantized per token.
 int self_attn_block(const qtx_config& c, const QLin& qkv, const QLin& o,
                     const float* const* ln, Scratch& s, int B, int S, const uint8_t* mask,
-                    long m_bs, long m_is, hipStream_t st) {
+                    long m_bs, long m_is, bool dec, hipStream_t st) {
   const int D = c.d_model, M = B * S;
   RC(ln_quant(s.x, M, ln, D, s.a8, s.sa, st));
   RC(linear(c, qkv, s.a8, s.sa, M, 0, nullptr, s.y, 3 * D, st));
@@ -808,6 +808,7 @@ int self_attn_block(const qtx_config& c, const QLin& qkv, const QLin& o,
   RC(quant(s.y + 2 * D, 3 * D, M, D, s.v8, s.sv, st));
   AttnArgs a = attn_args(s, B, S, S, S);
   a.mask = mask; a.m_bs = m_bs; a.m_is = m_is;
+  a.dec = dec;
   HIPCHK(launch_attention(a, st));
   RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
   RC(linear(c, o, s.a8, s.sa, M, EPI_RESIDUAL, s.x, s.x, D, st));
@@ -985,7 +986,7 @@ int encoder_run(const qtx_model* m, const float* x, const uint8_t* mask, int B, 
   if (x != s.x) HIPCHK(hipMemcpyAsync(s.x, x, (size_t)M * D * 4, hipMemcpyDeviceToDevice, st));
   if (!row_path(c)) {
     for (const EncLayer& L : m->enc) {
-      RC(self_attn_block(c, L.qkv, L.o, L.ln[0], s, B, S, mask, S, 0, st));
+      RC(self_attn_block(c, L.qkv, L.o, L.ln[0], s, B, S, mask, S, 0, false, st));
       RC(ffn_block(c, L.w1, L.w2, L.ln[1], s, M, st));
     }
     RC(ln_out(s.x, M, m->enc_norm, D, out, st));
@@ -1144,6 +1145,7 @@ int cross_attn_block(const qtx_model* m, const DecLayer& L, int l, Scratch& s,
   AttnArgs a = attn_args(s, B, T, S, S);
   a.k = x.k8[l]; a.sk = x.sk[l]; a.v = x.v8[l]; a.sv = x.sv[l];
   a.mask = src_mask; a.m_bs = S; a.m_is = 0;
+  a.dec = 1;
   HIPCHK(launch_attention(a, st));
   RC(quant(s.ctx, D, M, D, s.a8, s.sa, st));
   RC(linear(c, L.co, s.a8, s.sa, M, EPI_RESIDUAL, s.x, s.x, D, st));
@@ -1400,6 +1402,7 @@ int greedy_step_unfused(const qtx_model* m, GreedyWS& g, int B, int S, int max_l
     AttnArgs a = attn_args(s, B, 1, 0, max_len);
     a.k = g.kc[l]; a.sk = g.skc[l]; a.v = g.vc[l]; a.sv = g.svc[l];
     a.sk_dev = g.step; a.sk_add = 1;
+    a.dec = 1;
     HIPCHK(launch_attention(a, st));
     RC(quant(s.ctx, D, B, D, s.a8, s.sa, st));
     RC(linear(c, L.o, s.a8, s.sa, B, EPI_RESIDUAL, s.x, s.x, D, st));
@@ -1514,7 +1517,7 @@ int32_t qtx_decoder_forward_fault(const qtx_model* m, const float* y, const floa
   if (!row_path(c)) {
     for (int l = 0; l < c.n_layers; ++l) {
       const DecLayer& L = m->dec[l];
-      RC(self_attn_block(c, L.qkv, L.o, L.ln[0], s, B, T, tgt_mask, tm_bs, T, st));
+      RC(self_attn_block(c, L.qkv, L.o, L.ln[0], s, B, T, tgt_mask, tm_bs, T, true, st));
       RC(cross_attn_block(m, L, l, s, x, B, T, S, src_mask, st));
       RC(ffn_block(c, L.w1, L.w2, L.ln[2], s, M, st));
     }
@@ -1532,6 +1535,7 @@ int32_t qtx_decoder_forward_fault(const qtx_model* m, const float* y, const floa
     AttnArgs a = attn_args(s, B, T, T, T);
     a.mask = tgt_mask; a.m_bs = tm_bs; a.m_is = T;
     a.c_ld = D;
+    a.dec = 1;
     AttnFault af;
     if (attn_fault_for(f, 1, l, false, T, T, af)) {
       RC(attention_fault(a, af, M, D, s, st));
@@ -1550,6 +1554,7 @@ int32_t qtx_decoder_forward_fault(const qtx_model* m, const float* y, const floa
     a = attn_args(s, B, T, S, S);
     a.k = x.k8[l]; a.sk = x.sk[l]; a.v = x.v8[l]; a.sv = x.sv[l];
     a.mask = src_mask; a.m_bs = S; a.m_is = 0;
+    a.dec = 1;
     if (attn_fault_for(f, 1, l, true, T, S, af)) {
       RC(attention_fault(a, af, M, D, s, st));
     } else {
@@ -2024,7 +2029,7 @@ int32_t qtx_pack_int4(const int8_t* q, int32_t N, int32_t K, uint8_t* packed, vo
 int32_t qtx_attention_trace(const int8_t* q, const float* sq, const int8_t* k, const float* sk,
                             const int8_t* v, const float* sv, const uint8_t* mask, int64_t m_bs,
                             int64_t m_is, int32_t B, int32_t H, int32_t Sq, int32_t Sk,
-                            float* ctx, float* qk_acc, float* p_codes, void* stream) {
+                            float* ctx, float* qk_acc, float* p_codes, int32_t dec, void* stream) {
   if (!q || !sq || !k || !sk || !v || !sv || !ctx) return fail(QTX_E_INVALID, "null argument");
   if (Sk <= 0 || Sk > 512 || Sq <= 0 || B <= 0 || H <= 0)
     return fail(QTX_E_UNSUPPORTED, "Sk=%d (max 512) Sq=%d B=%d H=%d", Sk, Sq, B, H);
@@ -2036,6 +2041,7 @@ int32_t qtx_attention_trace(const int8_t* q, const float* sq, const int8_t* k, c
   a.mask = mask; a.m_bs = m_bs; a.m_is = m_is;
   a.ctx = ctx; a.c_bs = Sq * D; a.c_ld = D;
   a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
+  a.dec = dec != 0;
   HIPCHK(launch_attn_trace(a, qk_acc, p_codes, (hipStream_t)stream));
   return QTX_OK;
 }
@@ -2061,7 +2067,7 @@ int32_t qtx_attention_i8_quant(const int8_t* q, const float* sq, const int8_t* k
 int32_t qtx_attention_i8(const int8_t* q, const float* sq, const int8_t* k, const float* sk,
                          const int8_t* v, const float* sv, const uint8_t* mask, int64_t m_bs,
                          int64_t m_is, int32_t B, int32_t H, int32_t Sq, int32_t Sk,
-                         float* ctx, void* stream) {
+                         float* ctx, int32_t dec, void* stream) {
   if (!q || !sq || !k || !sk || !v || !sv || !ctx) return fail(QTX_E_INVALID, "null argument");
   if (Sk <= 0 || Sk > 512 || Sq <= 0) return fail(QTX_E_UNSUPPORTED, "Sk=%d (max 512)", Sk);
   const long D = (long)H * 64;
@@ -2072,6 +2078,7 @@ int32_t qtx_attention_i8(const int8_t* q, const float* sq, const int8_t* k, cons
   a.mask = mask; a.m_bs = m_bs; a.m_is = m_is;
   a.ctx = ctx; a.c_bs = Sq * D; a.c_ld = D;
   a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
+  a.dec = dec != 0;
   HIPCHK(launch_attention(a, (hipStream_t)stream));
   return QTX_OK;
 }

@@ -3,6 +3,8 @@
 //   s_ij = ((float(q_i . k_j) * s_q[i]) * s_k[j]) / 8     (exact int8 dot: MFMA i8)
 //   masked_fill(mask == 0, -1e9); P_ij = rint(softmax_j(s_ij) * 127) / 127
 //   ctx_id = fma chain over j = 0..Sk-1 of P_ij * (float(v_jd) * s_v[j])
+//            (a decoder layer's attention, a.dec: four chains over interleaved 4-key groups
+//            of fma(P_ij * s_v[j], float(v_jd), .), oracle attention_pv dec)
 //   attention.py:23-36 (per head, 64-wide), canonical order of oracle/qtx_oracle.py.
 //
 // The PV chain runs on v_mfma_f32_16x16x4f32: chained over k in order (C starts at 0) it
@@ -58,6 +60,7 @@ __device__ __forceinline__ float xmax32(float v) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+template <bool DEC>
 __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t Ks[AM_MAXK * 64];
   __shared__ __attribute__((aligned(16))) int8_t Vs[AM_MAXK * 64];
@@ -197,20 +200,27 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   QTX_STAMP(3);
 
   // ---- PV on fp32 MFMA: A = P[row fr][k] (the lane's x[s/4][s%4], k = 4s + fg),
-  // B = float(v[k][d]) * s_v[k] --------------------------------------------------------------
-  v4f acc[4] = {v4f{0, 0, 0, 0}, v4f{0, 0, 0, 0}, v4f{0, 0, 0, 0}, v4f{0, 0, 0, 0}};
+  // B = float(v[k][d]) * s_v[k].  DEC (the decoder's PV order, oracle attention_pv dec):
+  // A = RN(P * s_v[k]), B = float(v[k][d]), and step s goes to chain s & 3 — one MFMA step is
+  // one chain's 4 keys in order — the four chains summed (c0 + c1) + (c2 + c3) ----------------
+  constexpr int NCH = DEC ? 4 : 1;
+  v4f acc[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[c][dt] = v4f{0, 0, 0, 0};
   const uint32_t* vt32 = reinterpret_cast<const uint32_t*>(Vs);
 #pragma unroll
   for (int s4 = 0; s4 < 32; ++s4) {
     if (4 * s4 < nk4) {
       const int k = 4 * s4 + fg;
-      const float pa = x[s4 >> 2][s4 & 3];
       const float svk = svs[k];
+      const float pa = DEC ? x[s4 >> 2][s4 & 3] * svk : x[s4 >> 2][s4 & 3];
       const uint32_t vd = vt32[k * 16 + fr];
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const float vb2 = (float)(int8_t)(vd >> (8 * dt)) * svk;
-        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa, vb2, acc[dt], 0, 0, 0);
+        const float vb2 = DEC ? (float)(int8_t)(vd >> (8 * dt)) : (float)(int8_t)(vd >> (8 * dt)) * svk;
+        acc[s4 % NCH][dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa, vb2, acc[s4 % NCH][dt], 0, 0, 0);
       }
     }
   }
@@ -219,7 +229,9 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int row = r0 + 4 * fg + e;
-      if (row < Sq) a.ctx[b * a.c_bs + (long)row * a.c_ld + hoff + dt * 16 + fr] = acc[dt][e];
+      const float cv = DEC ? (acc[0][dt][e] + acc[1 % NCH][dt][e]) + (acc[2 % NCH][dt][e] + acc[3 % NCH][dt][e])
+                           : acc[0][dt][e];
+      if (row < Sq) a.ctx[b * a.c_bs + (long)row * a.c_ld + hoff + dt * 16 + fr] = cv;
     }
   QTX_STAMP(4);
 }
@@ -228,7 +240,10 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
 hipError_t launch_attention_mfma(const AttnArgs& a, hipStream_t st) {
   if (a.sk_dev || a.qpos_dev || a.H * 64 > 4096 || a.Sk <= 0 || a.Sk > AM_MAXK)
     return hipErrorNotSupported;
-  k_attn_mfma<<<dim3(a.H, a.B, (a.Sq + 63) / 64), dim3(256), 0, st>>>(a);
+  if (a.dec)
+    k_attn_mfma<true><<<dim3(a.H, a.B, (a.Sq + 63) / 64), dim3(256), 0, st>>>(a);
+  else
+    k_attn_mfma<false><<<dim3(a.H, a.B, (a.Sq + 63) / 64), dim3(256), 0, st>>>(a);
   return hipGetLastError();
 }
 
@@ -583,7 +598,7 @@ __global__ __launch_bounds__(512) void k_attn_encq(AttnArgs a, int8_t* ctx8, flo
 // stride a.c_ld, scales [B*S]); H == 8, Sq == Sk <= 128, per-key mask (m_is == 0).
 hipError_t launch_attention_encq(const AttnArgs& a, int8_t* ctx8, float* sctx, hipStream_t st,
                                  bool force_encq, bool kp) {
-  if (a.sk_dev || a.qpos_dev || a.H != 8 || a.Sk <= 0 || a.Sk > AM_MAXK || a.Sq != a.Sk ||
+  if (a.dec || a.sk_dev || a.qpos_dev || a.H != 8 || a.Sk <= 0 || a.Sk > AM_MAXK || a.Sq != a.Sk ||
       (a.mask && a.m_is != 0) || (a.k_ld % 16) || (a.v_ld % 16) || (a.c_ld % 4))
     return hipErrorNotSupported;
   if (a.B < 128 && !force_encq) return hipErrorNotSupported;   // one workgroup per sentence:
@@ -674,12 +689,19 @@ __global__ __launch_bounds__(64) void k_attn_fault_rows(AttnArgs a, AttnFault f)
   const int d = lane;
   const bool pin = f.kind == AF_PV_INPUT && i == f.i && d >= f.lo && d < f.hi;
   const bool vw = f.kind == AF_PV_WEIGHT && d == f.d && i >= f.lo && i < f.hi;
-  float acc = 0.0f;
-  for (int j = 0; j < Sk; ++j) {
+  auto vint = [&](int j) {
     const int8_t v8 = a.v[b * a.v_bs + (long)j * a.v_ld + hoff + d];
-    const int vv = (vw && j == f.j) ? flip(v8) : (int)v8;
-    const float vb = (float)vv * a.sv[b * a.sv_bs + j];
-    acc = fmaf(pin ? Pf[j] : Ps[j], vb, acc);
+    return (vw && j == f.j) ? flip(v8) : (int)v8;
+  };
+  float acc = 0.0f;
+  if (a.dec) {   // the decoder's PV order (qtx_common.h pv_dec_chains)
+    acc = pv_dec_chains(Sk, [&](int j) { return (pin ? Pf[j] : Ps[j]) * a.sv[b * a.sv_bs + j]; },
+                        [&](int j) { return (float)vint(j); });
+  } else {
+    for (int j = 0; j < Sk; ++j) {
+      const float vb = (float)vint(j) * a.sv[b * a.sv_bs + j];
+      acc = fmaf(pin ? Pf[j] : Ps[j], vb, acc);
+    }
   }
   if (f.kind == AF_PV_OUTPUT && i == f.i && d == f.d) acc = f.value;
   a.ctx[b * a.c_bs + (long)i * a.c_ld + hoff + d] = acc;
@@ -692,7 +714,8 @@ __global__ __launch_bounds__(64) void k_attn_fault_rows(AttnArgs a, AttnFault f)
 // canonical order of the oracle (attention_scores / softmax_quant / attention_pv):
 //   qk [B,H,Sq,Sk]  float(sum_d q[i][d] k[j][d])  (QK^T "FirstMatMul", exact integers)
 //   pc [B,H,Sq,Sk]  rint(P * 127)                 (the Round of attention.py:33-35)
-//   ctx             sum_j (P/127) v_j s_v[j] per head, as launch_attention writes it
+//   ctx             sum_j (P/127) v_j s_v[j] per head, as launch_attention writes it (a.dec:
+//                   the decoder's PV order)
 // Off the hot path (diagnostics / campaigns): scalar int8 loads, one row per wave.
 // =====================================================================================
 __global__ __launch_bounds__(64) void k_attn_trace(AttnArgs a, float* qk, float* pc) {
@@ -741,9 +764,14 @@ __global__ __launch_bounds__(64) void k_attn_trace(AttnArgs a, float* qk, float*
   __syncthreads();
   const int d = lane;
   float acc = 0.0f;
-  for (int j = 0; j < Sk; ++j) {
-    const float vb = (float)a.v[b * a.v_bs + (long)j * a.v_ld + hoff + d] * a.sv[b * a.sv_bs + j];
-    acc = fmaf(Ps[j], vb, acc);
+  if (a.dec) {   // the decoder's PV order (qtx_common.h pv_dec_chains)
+    acc = pv_dec_chains(Sk, [&](int j) { return Ps[j] * a.sv[b * a.sv_bs + j]; },
+                        [&](int j) { return (float)a.v[b * a.v_bs + (long)j * a.v_ld + hoff + d]; });
+  } else {
+    for (int j = 0; j < Sk; ++j) {
+      const float vb = (float)a.v[b * a.v_bs + (long)j * a.v_ld + hoff + d] * a.sv[b * a.sv_bs + j];
+      acc = fmaf(Ps[j], vb, acc);
+    }
   }
   a.ctx[b * a.c_bs + (long)i * a.c_ld + hoff + d] = acc;
 }

@@ -345,6 +345,24 @@ __device__ __forceinline__ int quant_one(float x, float s) {
   return (int)rintf(r);
 }
 
+// The decoder's PV order (oracle attention_pv dec) for one (query row, dim):
+// four chains, chain c over the keys j < Sk with (j >> 2) & 3 == c in key order, each
+// from +0, term fma(ps(j), v(j), acc_c) with ps(j) = RN(P_j * s_v[j]) and v(j) = float(v_jd)
+// supplied by the caller; summed (c0 + c1) + (c2 + c3).
+template <class PSF, class VF>
+__device__ __forceinline__ float pv_dec_chains(int Sk, PSF&& ps, VF&& v) {
+  float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int g = 0; g < Sk; g += 16)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = g + 4 * q + e;
+        if (j < Sk) c[q] = fmaf(ps(j), v(j), c[q]);
+      }
+  return (c[0] + c[1]) + (c[2] + c[3]);
+}
+
 // |x| as an order-preserving uint (for atomicMax on non-negative floats)
 __device__ __forceinline__ unsigned abs_bits(float x) { return __float_as_uint(fabsf(x)); }
 

@@ -666,7 +666,8 @@ template <bool KV_NEW, int NIT>
 __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   __shared__ uint32_t Ks[DEC_MAXK * 17];   // key rows of this head: 16 dwords (+1 pad)
   __shared__ __attribute__((aligned(16))) uint8_t Vs[DEC_MAXK * 64];
-  __shared__ float svs[DEC_MAXK], P[DEC_MAXK];
+  __shared__ float svs[DEC_MAXK];
+  __shared__ __attribute__((aligned(16))) float PS[DEC_MAXK];   // RN(P_j * s_v[j]), 0 past Sk
   __shared__ __attribute__((aligned(16))) int8_t qs[64];
   const int b = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
   QTX_STAMP(0);
@@ -803,22 +804,43 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   }
   // P = rint((e / den) * 127) / 127: e / den by div_cr, unguarded (den in [1, Sk]: the
   // row max contributes qexp(0) == 1; e >= 2^-60 gives the correctly rounded quotient and
-  // e < 2^-60 a P of 0 through either), / 127 by div127 — no true division per key
+  // e < 2^-60 a P of 0 through either), / 127 by div127 — no true division per key; the PV
+  // term's P * s_v once per key (the decoder's PV order, oracle attention_pv dec), and 0
+  // for the padded keys Sk .. nk16 - 1 of the last 16-key group
   const float den = wave_sum(lsum);
   const float rden = 1.0f / den;
+  const int nk16 = (Sk + 15) & ~15;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int j = lane + 64 * u;
-    if (j < Sk) P[j] = div127(rintf(div_cr(sc[u], den, rden) * 127.0f));
+    if (j < Sk) PS[j] = div127(rintf(div_cr(sc[u], den, rden) * 127.0f)) * svs[j];
+    else if (j < nk16) PS[j] = 0.0f;
   }
   __syncthreads();
   QTX_STAMP(2);
 
-  // phase 4: context dim h*64 + lane = sequential fma chain over the keys
-  float acc = 0.0f;
-#pragma unroll 8
-  for (int j = 0; j < Sk; ++j)
-    acc = fmaf(P[j], (float)(int8_t)Vs[j * 64 + lane] * svs[j], acc);
+  // phase 4: context dim h*64 + lane in the decoder's PV order: four chains, chain c over
+  // the keys j with (j >> 2) & 3 == c in key order, term fma(PS[j], float(v_j), acc_c),
+  // summed (c0 + c1) + (c2 + c3).  Per 16-key group the four chains' fmas are independent,
+  // so the lone wave's dependent chain is a quarter of the keys (it was one fma per key,
+  // 26-46 cycles each).  Padded keys: PS == 0 and a finite v, fma(0, v, acc) == acc.
+  float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
+  const int8_t* vl = reinterpret_cast<const int8_t*>(Vs) + lane;
+#pragma unroll 2
+  for (int g = 0; g < nk16; g += 16) {
+    const float4 p0 = *reinterpret_cast<const float4*>(PS + g);
+    const float4 p1 = *reinterpret_cast<const float4*>(PS + g + 4);
+    const float4 p2 = *reinterpret_cast<const float4*>(PS + g + 8);
+    const float4 p3 = *reinterpret_cast<const float4*>(PS + g + 12);
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = (float)vl[(g + e) * 64];
+    c0 = fmaf(p0.x, v[0], c0);  c1 = fmaf(p1.x, v[4], c1);  c2 = fmaf(p2.x, v[8], c2);  c3 = fmaf(p3.x, v[12], c3);
+    c0 = fmaf(p0.y, v[1], c0);  c1 = fmaf(p1.y, v[5], c1);  c2 = fmaf(p2.y, v[9], c2);  c3 = fmaf(p3.y, v[13], c3);
+    c0 = fmaf(p0.z, v[2], c0);  c1 = fmaf(p1.z, v[6], c1);  c2 = fmaf(p2.z, v[10], c2); c3 = fmaf(p3.z, v[14], c3);
+    c0 = fmaf(p0.w, v[3], c0);  c1 = fmaf(p1.w, v[7], c1);  c2 = fmaf(p2.w, v[11], c2); c3 = fmaf(p3.w, v[15], c3);
+  }
+  const float acc = (c0 + c1) + (c2 + c3);
   QTX_STAMP(3);
 
   // phase 5: this head's 64 context values (and their absmax when asked for: the consumer

@@ -95,6 +95,8 @@ struct AttnArgs {
   int B, H, Sq, Sk;                         // Sk: keys used (<= cached length)
   const int* sk_dev; int sk_add;            // if sk_dev: Sk = *sk_dev + sk_add (decode)
   const int* qpos_dev;                      // if set, query i's mask row = *qpos_dev + i
+  int dec;                                  // a decoder layer's attention: the decoder's PV
+                                            // order (oracle attention_pv dec)
 };
 
 // Fault in an attention MatMul of one (sentence b, head h) (k_attn_fault_rows): the

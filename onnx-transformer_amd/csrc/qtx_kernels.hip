@@ -286,7 +286,8 @@ hipError_t launch_gemm(const GemmArgs& g, int wbits, hipStream_t st) {
 // V and the key scales are staged once in LDS; each wave walks query rows.
 //   s_j  = ((float(sum_d q_d k_jd) * s_q) * s_k[j]) / 8      (exact int8 dot: v_dot4)
 //   mask -> -1e9;  e_j = qexp(s_j - max);  den = lane-split sum;  P_j = rint(e_j/den*127)/127
-//   ctx_d = fma chain over j of P_j * (float(v_jd) * s_v[j])
+//   ctx_d = fma chain over j of P_j * (float(v_jd) * s_v[j])  (a.dec: the decoder's order,
+//           pv_dec_chains)
 // =====================================================================================
 constexpr int ATT_MAXK = 512;
 
@@ -347,8 +348,13 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
     for (int j = lane; j < Sk; j += 64) P[j] = rintf((P[j] / den) * 127.0f) / 127.0f;
     __builtin_amdgcn_wave_barrier();
     float acc = 0.0f;
-    for (int j = 0; j < Sk; ++j)
-      acc = fmaf(P[j], (float)(int8_t)Vs[j * 64 + lane] * svs[j], acc);
+    if (a.dec) {   // the decoder's PV order (qtx_common.h pv_dec_chains)
+      acc = pv_dec_chains(Sk, [&](int j) { return P[j] * svs[j]; },
+                          [&](int j) { return (float)(int8_t)Vs[j * 64 + lane]; });
+    } else {
+      for (int j = 0; j < Sk; ++j)
+        acc = fmaf(P[j], (float)(int8_t)Vs[j * 64 + lane] * svs[j], acc);
+    }
     a.ctx[b * a.c_bs + (long)i * a.c_ld + hoff + lane] = acc;
     __builtin_amdgcn_wave_barrier();
   }

@@ -11,6 +11,15 @@
 // paths within one process call it after changing a variable.
 #pragma once
 
+// A diagnostic switch: a field read from the environment in the QTX_DIAG build, a
+// compile-time constant (its default) in the product build, so the product's branches on it
+// fold away and the library carries only the paths some shape takes by default.
+#ifdef QTX_DIAG
+#define QTX_DKNOB(T, name, def) T name = def
+#else
+#define QTX_DKNOB(T, name, def) static constexpr T name = def
+#endif
+
 namespace qtx {
 
 struct Knobs {
@@ -23,17 +32,8 @@ struct Knobs {
   bool enc_nosplit = false;  // QTX_ENC_NOSPLIT: no two-stream encoder (two-pass FFN1 only)
   bool unfused = false;      // QTX_UNFUSED: the unfused decoder step
   bool no_graph = false;     // QTX_NO_GRAPH: eager decode launches
-  bool group_graph = false;  // QTX_GROUP_GRAPH: sub-batches as branches of one graph
-  bool split_ln = false;     // QTX_SPLIT_LN: separate LayerNorm kernels in the decode step
   bool ffn_qkernel = false;  // QTX_FFN_QKERNEL: the FFN hidden quantized by its own kernel
-  bool ws_nopipe = false;    // QTX_WS_NOPIPE: the unpipelined weight-stationary kernel
-  bool wsr_off = false;      // QTX_WSR=0: the O-projection's WS epilogue on k_gemm_ws
-  bool attn_pmax = false;    // QTX_ATTN_PMAX: the decode O / Oc from the attention's per-head maxima
-  bool ffn_pmax = false;     // QTX_FFN_PMAX: the decode FFN2 from FFN1's per-tile maxima
-  bool hquant_rows = false;  // QTX_HQUANT_ROWS: the decode hidden quantized by k_rows
-  bool device_step = false;  // QTX_DEVICE_STEP: self-attention reads its position from the
-                             // device counter even where the host knows it
-  bool int4_packed = false;  // QTX_INT4_PACKED: a 4-bit model's decode step on the packed int4 kernels
+                             // (the default from B >= 96; forced below it by tests)
   int decode_groups = 0;     // QTX_DECODE_GROUPS: sub-batch graphs (0: by batch size)
   int graph_steps = 0;       // QTX_GRAPH_STEPS: decode steps per graph (0: all)
   long ws_min_m = 2048;      // QTX_WS_MIN_M: weight-stationary from this many rows
@@ -49,7 +49,20 @@ struct Knobs {
   int wsx_spin_limit = -1;   // QTX_WSX_SPIN_LIMIT: polls per wait (-1: the launcher's bound)
   int wsx_drop_slice = -1;   // QTX_WSX_DROP_SLICE: this column slice never publishes its
                              // row maxima, so its partners' waits time out (-1: none)
-  // ---- diagnostic switches (QTX_DIAG build only)
+  // ---- diagnostic switches (QTX_DIAG build only; constants in the product build)
+  // measured-negative decode / GEMM alternatives (round 6, VERDICT r05 item 5: moved out of
+  // the product; DESIGN.md records each A/B)
+  QTX_DKNOB(bool, group_graph, false);  // QTX_GROUP_GRAPH: sub-batches as branches of one graph
+  QTX_DKNOB(bool, split_ln, false);     // QTX_SPLIT_LN: separate LayerNorm kernels in the decode step
+  QTX_DKNOB(bool, ws_nopipe, false);    // QTX_WS_NOPIPE: the unpipelined weight-stationary kernel
+  QTX_DKNOB(bool, wsr_off, false);      // QTX_WSR=0: the O-projection's WS epilogue on k_gemm_ws
+  QTX_DKNOB(bool, attn_pmax, false);    // QTX_ATTN_PMAX: decode O / Oc from the attention's per-head maxima
+  QTX_DKNOB(bool, ffn_pmax, false);     // QTX_FFN_PMAX: decode FFN2 from FFN1's per-tile maxima
+  QTX_DKNOB(bool, hquant_rows, false);  // QTX_HQUANT_ROWS: the decode hidden quantized by k_rows
+  QTX_DKNOB(bool, device_step, false);  // QTX_DEVICE_STEP: self-attention reads its position from
+                                        // the device counter even where the host knows it
+  QTX_DKNOB(bool, int4_packed, false);  // QTX_INT4_PACKED: a 4-bit model's decode step on the
+                                        // packed int4 kernels
   int ablate = 0;            // QTX_ABLATE: kernel classes dropped from the decode step
   bool ablate_nop = false;   // QTX_ABLATE_NOP
   bool dbg_tail = false;     // QTX_DBG_TAIL

@@ -31,16 +31,7 @@ Knobs read_env() {
   k.enc_nosplit = flag("QTX_ENC_NOSPLIT");
   k.unfused = flag("QTX_UNFUSED");
   k.no_graph = flag("QTX_NO_GRAPH");
-  k.group_graph = flag("QTX_GROUP_GRAPH");
-  k.split_ln = flag("QTX_SPLIT_LN");
   k.ffn_qkernel = flag("QTX_FFN_QKERNEL");
-  k.ws_nopipe = flag("QTX_WS_NOPIPE");
-  k.wsr_off = getenv("QTX_WSR") && *getenv("QTX_WSR") == '0';
-  k.attn_pmax = flag("QTX_ATTN_PMAX");
-  k.ffn_pmax = flag("QTX_FFN_PMAX");
-  k.hquant_rows = flag("QTX_HQUANT_ROWS");
-  k.device_step = flag("QTX_DEVICE_STEP");
-  k.int4_packed = flag("QTX_INT4_PACKED");
   k.decode_groups = (int)num("QTX_DECODE_GROUPS", 0);
   k.graph_steps = (int)num("QTX_GRAPH_STEPS", 0);
   k.ws_min_m = num("QTX_WS_MIN_M", 2048L);
@@ -52,6 +43,15 @@ Knobs read_env() {
   k.wsx_spin_limit = (int)num("QTX_WSX_SPIN_LIMIT", -1);
   k.wsx_drop_slice = (int)num("QTX_WSX_DROP_SLICE", -1);
 #ifdef QTX_DIAG
+  k.group_graph = flag("QTX_GROUP_GRAPH");
+  k.split_ln = flag("QTX_SPLIT_LN");
+  k.ws_nopipe = flag("QTX_WS_NOPIPE");
+  k.wsr_off = getenv("QTX_WSR") && *getenv("QTX_WSR") == '0';
+  k.attn_pmax = flag("QTX_ATTN_PMAX");
+  k.ffn_pmax = flag("QTX_FFN_PMAX");
+  k.hquant_rows = flag("QTX_HQUANT_ROWS");
+  k.device_step = flag("QTX_DEVICE_STEP");
+  k.int4_packed = flag("QTX_INT4_PACKED");
   k.ablate = (int)num("QTX_ABLATE", 0);
   k.ablate_nop = flag("QTX_ABLATE_NOP");
   k.dbg_tail = flag("QTX_DBG_TAIL");

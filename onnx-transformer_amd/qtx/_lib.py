@@ -89,8 +89,8 @@ SIGNATURES = {
     "qtx_ffn_rows": (I32, [C.POINTER(FfnRows), P]),
     "qtx_pack_ffn": (I32, [P, P, I32, P, P]),
     "qtx_pack_int4": (I32, [P, I32, I32, P, P]),
-    "qtx_attention_i8": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, P]),
-    "qtx_attention_trace": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, P, P, P]),
+    "qtx_attention_i8": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, I32, P]),
+    "qtx_attention_trace": (I32, [P, P, P, P, P, P, P, I64, I64, I32, I32, I32, I32, P, P, P, I32, P]),
     "qtx_attention_i8_quant": (I32, [P, P, P, P, P, P, P, I32, I32, P, P, P]),
     "qtx_skinny_linear": (I32, [I32, P, P, P, I64, P, P, P, I32, P, P, P, I32, I32, I32, I32,
                                 I32, P, P, P, P]),

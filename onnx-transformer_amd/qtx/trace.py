@@ -153,16 +153,16 @@ class _Tracer:
         self.out[f"Round_{n}_out0"] = w.float().t().contiguous().cpu().numpy()
         self.out[f"Round_{n}_scale"] = _view(torch, sw.value, (N,), "<f4", self.dev).cpu().numpy()
 
-    def attention(self, q, sq, k, sk, v, sv, mask, m_bs, m_is, B, Sq, Sk, names):
+    def attention(self, q, sq, k, sk, v, sv, mask, m_bs, m_is, B, Sq, Sk, names, dec=False):
         """Attention core with its intermediates stored under names = (Round of P,
-        MatMul QK^T, MatMul PV)."""
+        MatMul QK^T, MatMul PV); dec: a decoder layer's (the decoder's PV order)."""
         H = 8
         ctx = self.empty(B * Sq, D)
         qk = self.empty(B, H, Sq, Sk)
         pc = self.empty(B, H, Sq, Sk)
         _lib.call("qtx_attention_trace", _ptr(q), _ptr(sq), _ptr(k), _ptr(sk), _ptr(v),
                   _ptr(sv), _ptr(mask), m_bs, m_is, B, H, Sq, Sk, _ptr(ctx), _ptr(qk), _ptr(pc),
-                  self.st)
+                  int(dec), self.st)
         p_n, qk_n, pv_n = names
         self.out[f"Round_{p_n}_out0"] = pc.cpu().numpy()
         self.out[f"Round_{p_n}_scale"] = np.float32(1.0) / np.float32(127.0)
@@ -253,7 +253,7 @@ def trace_decoder(model, y, memory, src_mask_u8, tgt_mask_u8, weights: bool = Fa
             q, s = t.quant(yy, M, D)
             t.put_codes(act[n.lower()], q, s, shp)
             qkv += [q, s]
-        ctx = t.attention(*qkv, tm, tm_bs, T, B, T, T, (act["P"], mm["QK"], mm["PV"]))
+        ctx = t.attention(*qkv, tm, tm_bs, T, B, T, T, (act["P"], mm["QK"], mm["PV"]), dec=True)
         cq, cs = t.quant(ctx, M, D)
         t.put_codes(act["ctx"], cq, cs, shp)
         x = t.gemm(cq, cs, t.linear(1, L, 3), M, flags=2, res=x, mm=mm["O"], wname=wt["O"],
@@ -270,7 +270,7 @@ def trace_decoder(model, y, memory, src_mask_u8, tgt_mask_u8, weights: bool = Fa
             kq, ks = t.quant(yy, Mm, D)
             t.put_codes(act["c_k" if n == "CK" else "c_v"], kq, ks, mshp)
             kv += [kq, ks]
-        ctx = t.attention(q, qs, *kv, sm, S, 0, B, T, S, (act["c_P"], mm["CQK"], mm["CPV"]))
+        ctx = t.attention(q, qs, *kv, sm, S, 0, B, T, S, (act["c_P"], mm["CQK"], mm["CPV"]), dec=True)
         cq, cs = t.quant(ctx, M, D)
         t.put_codes(act["c_ctx"], cq, cs, shp)
         x = t.gemm(cq, cs, t.linear(1, L, 7), M, flags=2, res=x, mm=mm["CO"], wname=wt["CO"],

@@ -12,7 +12,8 @@ The canonical order is the contract the HIP kernels implement, so the GPU path a
 oracle agree bit-for-bit (see DESIGN.md §3 "numerics contract"):
 
 * no FMA contraction except where the canonical order says ``fma`` (PV and generator dots;
-  the generator's dot as four partial chains over k-quarters, summed pairwise);
+  the generator's dot as four partial chains over k-quarters, summed pairwise; the
+  decoder's PV as four partial chains over interleaved 4-key groups, attention_pv);
 * LayerNorm / softmax / log-softmax sums use a fixed lane-split + xor-butterfly tree;
 * softmax uses :func:`qexp`, a fixed polynomial exp that both sides evaluate identically.
 
@@ -298,15 +299,35 @@ def softmax_quant(scores):
     return np.rint(p * f32(127.0)).astype(np.int8)
 
 
-def attention_pv(qp, qv, sv):
-    """ctx[b,h,i,d] = fma chain over j of (qp/127) * (float(qv) * s_v[j])."""
+def attention_pv(qp, qv, sv, dec=False):
+    """The PV MatMul (attention.py:36) in the canonical order.
+
+    Encoder (dec=False): ctx[b,h,i,d] = one fma chain over j in key order, from 0, of
+    (qp/127) * (float(qv) * s_v[j]).
+
+    Decoder (dec=True, round 6; self and cross attention of decoder.py:28-33): four partial
+    chains — chain c takes the keys j with (j >> 2) & 3 == c, in key order, from 0 — of the
+    term fma(RN(P_j * s_v[j]), float(v_jd), acc_c), summed ((c0 + c1) + (c2 + c3)).  The
+    decode step runs its PV as one lane per head dim (qtx_decode.hip k_dec_attn), where the
+    single chain was a dependent fma per key; the chain split (keys 4 at a time, so one
+    v_mfma_f32_16x16x4f32 step of the decoder-module kernel is one chain's 4 keys) and the
+    per-key P * s_v product (one multiply per key instead of one per key and dim) shorten it.
+    Same reference arithmetic (P @ (v * s_v) in fp32), a different rounding order."""
     P = qp.astype(f32) / f32(127.0)                                 # [B,H,Sq,Sk]
-    V = qv.astype(f32) * np.asarray(sv, f32)[:, None, :, None]      # [B,H,Sk,dk]
     B, H, Sq, Sk = P.shape
-    acc = np.zeros((B, H, Sq, V.shape[-1]), f32)
+    if not dec:
+        V = qv.astype(f32) * np.asarray(sv, f32)[:, None, :, None]  # [B,H,Sk,dk]
+        acc = np.zeros((B, H, Sq, V.shape[-1]), f32)
+        for j in range(Sk):
+            acc = fma32(P[..., j, None], V[:, :, j, None, :], acc)
+        return acc
+    PS = (P * np.asarray(sv, f32)[:, None, None, :]).astype(f32)   # RN(P_j * s_v[j])
+    V = qv.astype(f32)                                              # exact
+    acc = [np.zeros((B, H, Sq, V.shape[-1]), f32) for _ in range(4)]
     for j in range(Sk):
-        acc = fma32(P[..., j, None], V[:, :, j, None, :], acc)
-    return acc
+        c = (j >> 2) & 3
+        acc[c] = fma32(PS[..., j, None], V[:, :, j, None, :], acc[c])
+    return ((acc[0] + acc[1]) + (acc[2] + acc[3])).astype(f32)
 
 
 def split_heads(q, H):
@@ -324,8 +345,9 @@ def _flip8(v, bit):
     return np.int8(np.uint8(np.int8(v).view(np.uint8) ^ (1 << int(bit))).view(np.int8))
 
 
-def attention(qq, sq, qk, sk, qv, sv, mask, H=8, fault=None):
+def attention(qq, sq, qk, sk, qv, sv, mask, H=8, fault=None, dec=False):
     """Quantized Q/K/V [B,S,512] int8 + per-token scales -> ctx [B,Sq,512] f32, P ints.
+    dec: the decoder's PV order (attention_pv).
 
     fault (fault-injection runs, one (sentence b, head h)): dict with kind QK_INPUT /
     QK_WEIGHT / QK_OUTPUT / PV_INPUT / PV_WEIGHT / PV_OUTPUT and b, h, i, j, d, lo, hi,
@@ -338,7 +360,7 @@ def attention(qq, sq, qk, sk, qv, sv, mask, H=8, fault=None):
     if fault is None:
         scores = attention_scores(q4, sq, k4, sk, mask)
         qp = softmax_quant(scores)
-        ctx = attention_pv(qp, v4, sv)
+        ctx = attention_pv(qp, v4, sv, dec)
         return merge_heads(ctx), qp
     kind, b, h = fault["kind"], fault["b"], fault["h"]
     i, j, d, lo, hi, bit = (fault[k] for k in ("i", "j", "d", "lo", "hi", "bit"))
@@ -358,16 +380,16 @@ def attention(qq, sq, qk, sk, qv, sv, mask, H=8, fault=None):
     keep = np.broadcast_to(np.asarray(mask) != 0, (q4.shape[0], q4.shape[2], k4.shape[2]))
     scores = np.where(keep[:, None], s, MASK_FILL).astype(f32)
     qp = softmax_quant(scores)
-    ctx = attention_pv(qp, v4, sv)
+    ctx = attention_pv(qp, v4, sv, dec)
     if kind == "PV_INPUT":
         qp2 = qp[b:b + 1, h:h + 1].copy()
         qp2[0, 0, i, j] = _flip8(qp2[0, 0, i, j], bit)
-        c2 = attention_pv(qp2, v4[b:b + 1, h:h + 1], np.asarray(sv)[b:b + 1])
+        c2 = attention_pv(qp2, v4[b:b + 1, h:h + 1], np.asarray(sv)[b:b + 1], dec)
         ctx[b, h, i, lo:hi] = c2[0, 0, i, lo:hi]
     elif kind == "PV_WEIGHT":
         v2 = v4[b:b + 1, h:h + 1].copy()
         v2[0, 0, j, d] = _flip8(v2[0, 0, j, d], bit)
-        c2 = attention_pv(qp[b:b + 1, h:h + 1], v2, np.asarray(sv)[b:b + 1])
+        c2 = attention_pv(qp[b:b + 1, h:h + 1], v2, np.asarray(sv)[b:b + 1], dec)
         ctx[b, h, lo:hi, d] = c2[0, 0, lo:hi, d]
     elif kind == "PV_OUTPUT":
         ctx[b, h, i, d] = f32(fault["value"])
@@ -463,12 +485,13 @@ class OracleModel:
                                 else (0, Sq))
         return f
 
-    def mha(self, lin, xq, xkv, mask, faults=(None,) * 4, attn_fault=None):
-        """MultiHeadedAttention.forward (attention.py:39-67)."""
+    def mha(self, lin, xq, xkv, mask, faults=(None,) * 4, attn_fault=None, dec=False):
+        """MultiHeadedAttention.forward (attention.py:39-67); dec: a decoder layer's
+        attention (the decoder's PV order, attention_pv)."""
         qq, sq = lin[0](xq, quantize_output=True, fault=faults[0])
         qk, sk = lin[1](xkv, quantize_output=True, fault=faults[1])
         qv, sv = lin[2](xkv, quantize_output=True, fault=faults[2])
-        ctx, _ = attention(qq, sq, qk, sk, qv, sv, mask, self.H, fault=attn_fault)
+        ctx, _ = attention(qq, sq, qk, sk, qv, sv, mask, self.H, fault=attn_fault, dec=dec)
         return lin[3](ctx, fault=faults[3])
 
     def ffn(self, lp, x, faults=(None, None)):
@@ -505,11 +528,11 @@ class OracleModel:
             h = layer_norm(x, *lp["ln"][0])
             T, S = x.shape[1], np.asarray(memory).shape[1]
             x = x + self.mha(lp["self_attn"], h, h, tm, [lf("Q"), lf("K"), lf("V"), lf("O")],
-                             self._attn_fault(fault, 1, L, "QK", "PV", T, T))
+                             self._attn_fault(fault, 1, L, "QK", "PV", T, T), dec=True)
             h = layer_norm(x, *lp["ln"][1])
             x = x + self.mha(lp["src_attn"], h, memory, sm,
                              [lf("CQ"), lf("CK", mrows), lf("CV", mrows), lf("CO")],
-                             self._attn_fault(fault, 1, L, "CQK", "CPV", T, S))
+                             self._attn_fault(fault, 1, L, "CQK", "CPV", T, S), dec=True)
             x = x + self.ffn(lp, layer_norm(x, *lp["ln"][2]),
                              [lf("FFN1", rows, lp["w1"].q.shape[0]), lf("FFN2")])
         return layer_norm(x, *self.dec_norm)
@@ -602,13 +625,13 @@ class DecodeState:
                 self.vcache[L] = tuple(np.concatenate([a, b], 1) for a, b in zip(self.vcache[L], v))
             (qk, sk), (qv, sv) = self.kcache[L], self.vcache[L]
             ones = np.ones((B, 1, qk.shape[1]), np.int64)
-            ctx, _ = attention(qq, sq, qk, sk, qv, sv, ones, m.H)
+            ctx, _ = attention(qq, sq, qk, sk, qv, sv, ones, m.H, dec=True)
             x = x + lin[3](ctx)
             h = layer_norm(x, *lp["ln"][1])
             lin = lp["src_attn"]
             qq, sq = lin[0](h, quantize_output=True)
             (qk, sk), (qv, sv) = self.cross[L]
-            ctx, _ = attention(qq, sq, qk, sk, qv, sv, self.sm, m.H)
+            ctx, _ = attention(qq, sq, qk, sk, qv, sv, self.sm, m.H, dec=True)
             x = x + lin[3](ctx)
             x = x + m.ffn(lp, layer_norm(x, *lp["ln"][2]))
         return layer_norm(x, *m.dec_norm)[:, 0]

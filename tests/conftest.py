@@ -15,6 +15,26 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm gfx950 GPU (MI355X)")
+    config.addinivalue_line("markers", "diag: forces a diagnostic switch (csrc/qtx_knobs.h "
+                            "QTX_DKNOB): runs only against libqtx_diag.so, in the subprocess "
+                            "of tests/test_diag_build.py::test_diag_switch_paths")
+
+
+def _diag_lib():
+    return "diag" in os.path.basename(os.environ.get("QTX_LIB_PATH", ""))
+
+
+def pytest_collection_modifyitems(config, items):
+    """The product library reads no diagnostic switch (they are constants there), so a test
+    that forces one would silently run the default path: such tests (marker diag) run only
+    in the process test_diag_build.py starts with QTX_LIB_PATH = libqtx_diag.so."""
+    if _diag_lib():
+        return
+    skip = pytest.mark.skip(reason="diag switch: run against libqtx_diag.so by "
+                                   "tests/test_diag_build.py::test_diag_switch_paths")
+    for it in items:
+        if "diag" in it.keywords:
+            it.add_marker(skip)
 
 
 @pytest.fixture(scope="session")

@@ -125,9 +125,9 @@ def enc_layer(om, lp, y, m):
 def dec_layer(om, lp, y, mem, sm, tm):
     """DecoderLayer.forward (decoder.py:28-33) in the oracle."""
     h = O.layer_norm(y, *lp["ln"][0])
-    y = y + om.mha(lp["self_attn"], h, h, tm)
+    y = y + om.mha(lp["self_attn"], h, h, tm, dec=True)
     h = O.layer_norm(y, *lp["ln"][1])
-    y = y + om.mha(lp["src_attn"], h, mem, sm)
+    y = y + om.mha(lp["src_attn"], h, mem, sm, dec=True)
     return y + om.ffn(lp, O.layer_norm(y, *lp["ln"][2]))
 
 

@@ -41,3 +41,25 @@ def test_diag_variants_bit_exact():
                        capture_output=True, text=True, env=env, timeout=300)
     print(r.stdout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+@pytest.mark.gpu
+def test_diag_switch_paths():
+    """The tests that force a diagnostic switch (marker diag: the measured-negative decode
+    and GEMM alternatives of csrc/qtx_knobs.h QTX_DKNOB, constants in libqtx.so) run in one
+    subprocess against libqtx_diag.so, where the switches are read."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if not os.path.exists(DIAG_LIB):
+        sys.path.insert(0, os.path.join(REPO, "onnx-transformer_amd"))
+        from qtx import _build
+        _build.build(extra=["-DQTX_DIAG"])
+    env = dict(os.environ, QTX_LIB_PATH=DIAG_LIB)
+    r = subprocess.run([sys.executable, "-u", "-m", "pytest", os.path.join(REPO, "tests"), "-q",
+                        "-m", "gpu and diag", "-p", "no:cacheprovider", "--timeout", "120",
+                        "--timeout-method", "thread"],
+                       capture_output=True, text=True, env=env, timeout=600, cwd=REPO)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert " passed" in r.stdout and " skipped" not in r.stdout.splitlines()[-1], r.stdout[-500:]

@@ -159,10 +159,9 @@ def test_cfg5_greedy_256_equals_batches_of_32(torch, gpu_model, oracle_model):
                                       oracle_model.greedy_decode(src[b:b + 1], m[b:b + 1], 72))
 
 
-def test_cfg4_int4_greedy_b32_matches_oracle(torch, state_dict, knob_env):
+def test_cfg4_int4_greedy_b32_matches_oracle(torch, state_dict):
     """The 4-bit model's decode (its weights unpacked to int8 for the step kernels) equals
-    the oracle on a sample; the step on the packed int4 kernels (QTX_INT4_PACKED) gives the
-    same ids for the whole batch."""
+    the oracle on a sample."""
     from qtx.decode import greedy_decode
     from qtx.model import QtxModel
     from qtx.weights import ModelConfig
@@ -172,11 +171,23 @@ def test_cfg4_int4_greedy_b32_matches_oracle(torch, state_dict, knob_env):
     o4 = O.OracleModel(state_dict, n_bits=4)
     pick = np.array([0, 9, 20, 31])
     np.testing.assert_array_equal(ys[pick], o4.greedy_decode(src[pick], m[pick], 72))
-    knob_env("QTX_INT4_PACKED", 1)
-    np.testing.assert_array_equal(greedy_decode(m4, src, m, 72, 0), ys)
     # the int4 model is a different model: its tokens differ from the int8 ones
     ys8 = greedy_decode(QtxModel(state_dict), src[:4], m[:4], 72, 0)
     assert (ys8 != ys[:4]).any()
+
+
+@pytest.mark.diag
+def test_cfg4_int4_packed_step_same_ids(torch, state_dict, knob_env):
+    """The diagnostic build's decode step on the packed int4 kernels (QTX_INT4_PACKED,
+    measured 5.7 % slower) gives the unpacked step's ids for the whole batch."""
+    from qtx.decode import greedy_decode
+    from qtx.model import QtxModel
+    from qtx.weights import ModelConfig
+    m4 = QtxModel(state_dict, ModelConfig(weight_bits=4))
+    src, m = _cfg2_src(404, 32)
+    ys = greedy_decode(m4, src, m, 72, 0)
+    knob_env("QTX_INT4_PACKED", 1)
+    np.testing.assert_array_equal(greedy_decode(m4, src, m, 72, 0), ys)
 
 
 def test_greedy_fresh_buffers_reuse_graph(torch, gpu_model):

@@ -181,7 +181,7 @@ def test_decode_self_attention(torch, B, step, kv_bs):
     np.testing.assert_array_equal(skd.cpu().numpy(), skc)
     n = step + 1
     ctx, _ = O.attention(qq[:, None], sq[:, None], kc[:, :n], skc[:, :n], vc[:, :n],
-                         svc[:, :n], np.ones((B, 1, n), np.uint8))
+                         svc[:, :n], np.ones((B, 1, n), np.uint8), dec=True)
     np.testing.assert_array_equal(ctxd.cpu().numpy(), ctx[:, 0])
     np.testing.assert_array_equal(pm.cpu().numpy(), head_max(ctx[:, 0]))
 
@@ -210,7 +210,7 @@ def test_decode_cross_attention(torch, B, S, holes):
          P(dev(torch, skc)), P(dev(torch, svc)), S, S0, S, P(dev(torch, mask)), B, P(ctxd),
          P(pm), S0)
     qq, sq = O.quant_rows(y)
-    ctx, _ = O.attention(qq[:, None], sq[:, None], kc, skc, vc, svc, mask[:, None])
+    ctx, _ = O.attention(qq[:, None], sq[:, None], kc, skc, vc, svc, mask[:, None], dec=True)
     np.testing.assert_array_equal(ctxd.cpu().numpy(), ctx[:, 0])
     np.testing.assert_array_equal(pm.cpu().numpy(), head_max(ctx[:, 0]))
 

@@ -67,10 +67,7 @@ def test_greedy_decode_matches_oracle(torch, gpu_model, oracle_model, golden_mod
 @pytest.mark.parametrize("env", [{"QTX_NO_GRAPH": "1"}, {"QTX_UNFUSED": "1"},
                                  {"QTX_GRAPH_STEPS": "13"}, {"QTX_DECODE_GROUPS": "3"},
                                  {"QTX_DECODE_GROUPS": "2", "QTX_NO_GRAPH": "1"},
-                                 {"QTX_DECODE_GROUPS": "2", "QTX_GROUP_GRAPH": "1"},
-                                 {"QTX_SPLIT_LN": "1"}, {"QTX_FFN_QKERNEL": "1"},
-                                 {"QTX_DEVICE_STEP": "1"}, {"QTX_ATTN_PMAX": "1"},
-                                 {"QTX_FFN_PMAX": "1"}, {"QTX_HQUANT_ROWS": "1"}])
+                                 {"QTX_FFN_QKERNEL": "1"}])
 def test_greedy_paths_agree(torch, gpu_model, knob_env, env):
     """The fused+graph decode step, the fused eager step, the unfused kernels, graphs of
     several steps and sub-batches on several streams agree."""
@@ -80,6 +77,19 @@ def test_greedy_paths_agree(torch, gpu_model, knob_env, env):
     for k, v in env.items():
         knob_env(k, v)
     np.testing.assert_array_equal(greedy_decode(gpu_model, src, m, 40, 0), ref)
+
+
+@pytest.mark.diag
+@pytest.mark.parametrize("env", [{"QTX_DECODE_GROUPS": "2", "QTX_GROUP_GRAPH": "1"},
+                                 {"QTX_SPLIT_LN": "1"}, {"QTX_DEVICE_STEP": "1"},
+                                 {"QTX_ATTN_PMAX": "1"}, {"QTX_FFN_PMAX": "1"},
+                                 {"QTX_HQUANT_ROWS": "1"}])
+def test_greedy_diag_paths_agree(torch, gpu_model, knob_env, env):
+    """The measured-negative decode alternatives of the diagnostic build (csrc/qtx_knobs.h
+    QTX_DKNOB: one graph with sub-batch branches, separate LayerNorm kernels, the device
+    position counter, per-head / per-tile partial maxima, the hidden quantized by k_rows)
+    give the product step's ids."""
+    test_greedy_paths_agree(torch, gpu_model, knob_env, env)
 
 
 def test_greedy_default_groups_at_512(torch, gpu_model, knob_env):

@@ -135,7 +135,10 @@ def test_linear_asymmetric_identity(torch, M):
                                             (3, 128, 128, "key"), (2, 72, 72, "key"),
                                             (2, 65, 100, "key"), (2, 16, 64, "key"),
                                             (1, 130, 5, "key")])
-def test_attention(torch, B, Sq, Sk, masked):
+@pytest.mark.parametrize("dec", [0, 1])
+def test_attention(torch, B, Sq, Sk, masked, dec):
+    """qtx_attention_i8 == oracle attention, in the encoder's PV order (dec 0) and the
+    decoder's (dec 1: four partial chains; k_attn_mfma<true>, and k_attention past 128 keys)."""
     rng = np.random.default_rng(Sq * 7 + Sk)
     H = 8
     q = rng.integers(-127, 128, (B, Sq, 512)).astype(np.int8)
@@ -156,8 +159,8 @@ def test_attention(torch, B, Sq, Sk, masked):
     ctx = torch.empty((B, Sq, 512), dtype=torch.float32, device="cuda")
     call("qtx_attention_i8", P(dev(torch, q)), P(dev(torch, sq)), P(dev(torch, k)),
          P(dev(torch, sk)), P(dev(torch, v)), P(dev(torch, sv)), P(dev(torch, mdev)),
-         m_bs, m_is, B, H, Sq, Sk, P(ctx), S0)
-    co, _ = O.attention(q, sq, k, sk, v, sv, mask, H)
+         m_bs, m_is, B, H, Sq, Sk, P(ctx), dec, S0)
+    co, _ = O.attention(q, sq, k, sk, v, sv, mask, H, dec=bool(dec))
     np.testing.assert_array_equal(ctx.cpu().numpy(), co)
 
 
@@ -534,7 +537,9 @@ def test_pack_w_ws(torch):
     assert lib().qtx_pack_w_ws(P(dev(torch, w)), 1024, 256, P(out), S0) != 0   # K != 512
 
 
-@pytest.mark.parametrize("M,nopipe", [(300, 0), (7, 0), (64, 0), (20011, 0), (20011, 1), (300, 1)])
+@pytest.mark.parametrize("M,nopipe", [(300, 0), (7, 0), (64, 0), (20011, 0),
+                                     pytest.param(20011, 1, marks=pytest.mark.diag),
+                                     pytest.param(300, 1, marks=pytest.mark.diag)])
 def test_linear_rows_ws(torch, oracle_model, knob_env, M, nopipe):
     """kp = 2 (weight-stationary, K = 512): every epilogue bit-exact against the oracle —
     Q/K/V per-token quant (row-major out), FFN1 row maxima + hidden quant (KP out), O-proj

@@ -26,7 +26,7 @@ sc = torch.empty((B, S), device="cuda")
 
 
 def old():
-    L.qtx_attention_i8(P(q), P(sq), P(k), P(sk), P(v), P(sv), P(km), S, 0, B, 8, S, S, P(ctx), S0)
+    L.qtx_attention_i8(P(q), P(sq), P(k), P(sk), P(v), P(sv), P(km), S, 0, B, 8, S, S, P(ctx), 0, S0)
 
 
 def new():

@@ -170,10 +170,131 @@ __global__ __launch_bounds__(NW * 64) void k_ring(const int8_t* W, int* sink, un
   if (tid == 0) { out[blockIdx.x * 2] = t1 - t0; out[blockIdx.x * 2 + 1] = r1 - r0; }
 }
 
+// ---- round 6: the ring the guide measures (MI355X_MICROARCH.md
+// ring-gemm) — dedicated loader waves and per-slot FULL / FREE words in LDS, no s_barrier.
+// NC consumer waves (each 128 / NC rows of the block: RF = 8 / NC row fragments, so every
+// fragment it reads feeds RF MFMAs) + NL loader waves (no compute).  The same 3 MB per CU
+// (pass 1's W1 + pass 2's W1 / W2 interleaved, per-CU rotation), in SLOTKB-KB slots.
+//   loader l, stream slot j: wait until every consumer has released slot j - NSLOT (its FREE
+//     word >= j - NSLOT), issue its SLOTKB / NL pieces, then publish slot j - D (its FULL
+//     word = j - D) behind s_waitcnt vmcnt(D * pieces): the loop holds no memory op but
+//     the DMAs, so the counted wait is exact (VM_CNT_ORDER); D slots stay in flight.
+//   consumer c, slot s: poll the NL FULL words (one lane each) until all >= s, read the
+//     slot's fragments into registers, s_waitcnt lgkmcnt(0), write its FREE word = s, then
+//     the MFMAs (the next slot's poll and reads issue under them).
+// MODE 0 fill + consume, 1 loaders only (consumers release at once, read nothing),
+// 2 consumers only (the FULL words pre-set, no DMA).
+template <int NC, int NL, int NSLOT, int SLOTKB, int D, int MODE, bool NT>
+__global__ __launch_bounds__((NC + NL) * 64) void k_ring2(const int8_t* W, int* sink, unsigned long long* out) {
+  constexpr int SL = SLOTKB * 1024;
+  constexpr int NS = 3 * NCHUNK * SLOT / SL;          // stream slots per block (3 MB)
+  constexpr int FR = SLOTKB;                          // 1 KB fragments per slot
+  constexpr int PPL = FR / NL;                        // pieces per loader per slot
+  constexpr int RF = 8 / NC;                          // row fragments per consumer
+  static_assert(FR % NL == 0 && 8 % NC == 0 && D + 1 < NSLOT, "shape");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NSLOT * SL];
+  __shared__ int fullw[NSLOT][NL];
+  __shared__ int freew[NSLOT][NC];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int rot = (int)((blockIdx.x >> 3) * 5 + (blockIdx.x & 7) * 3) % NCHUNK;
+  // stream slot j -> its byte offset in the 2 MB region (32 KB units as k_ring, split)
+  auto src_off = [&](int j) {
+    constexpr int SUB = SLOT / SL;                    // stream slots per 32 KB unit
+    const int u = j / SUB, part = j % SUB;
+    const int pass2 = u >= NCHUNK;
+    const int c0 = pass2 ? (u - NCHUNK) >> 1 : u;
+    const int c = (c0 + rot) % NCHUNK;
+    const int unit = pass2 ? 2 * c + ((u - NCHUNK) & 1) : 2 * c;
+    return (long)unit * SLOT + (long)part * SL;
+  };
+  for (int i = tid; i < NSLOT * NL; i += (NC + NL) * 64) (&fullw[0][0])[i] = MODE == 2 ? 1 << 30 : -1;
+  for (int i = tid; i < NSLOT * NC; i += (NC + NL) * 64) (&freew[0][0])[i] = -1;
+  __syncthreads();
+  volatile int* vfull = &fullw[0][0];
+  volatile int* vfree = &freew[0][0];
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  int sum = 0;
+  if (wave >= NC) {
+    // ---------------- loader
+    const int l = wave - NC;
+    if constexpr (MODE != 2) {
+      for (int j = 0; j < NS; ++j) {
+        const int slot = j % NSLOT;
+        if (j >= NSLOT) {
+          while (true) {
+            const int v = lane < NC ? vfree[slot * NC + lane] : j;
+            if (__builtin_amdgcn_ballot_w64(v < j - NSLOT) == 0ull) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        const int8_t* src = W + src_off(j) + (l * PPL) * 1024 + lane * 16;
+        uint8_t* dst = lds + slot * SL + (l * PPL) * 1024;
+#pragma unroll
+        for (int p = 0; p < PPL; ++p) dma16<NT>(src + p * 1024, dst + p * 1024);
+        if (j >= D) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D * PPL) : "memory");
+          if (lane == 0) vfull[((j - D) % NSLOT) * NL + l] = j - D;
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        for (int j = (NS > D ? NS - D : 0); j < NS; ++j) vfull[(j % NSLOT) * NL + l] = j;
+    }
+  } else {
+    // ---------------- consumer
+    const int c = wave;
+    v4i xa[RF][8];
+#pragma unroll
+    for (int i = 0; i < RF; ++i)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) xa[i][k] = v4i{tid + i, k, lane * 3, i ^ k};
+    v4i acc[RF][8];
+#pragma unroll
+    for (int i = 0; i < RF; ++i)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[i][k] = v4i{0, 0, 0, 0};
+    for (int s = 0; s < NS; ++s) {
+      const int slot = s % NSLOT;
+      if constexpr (MODE != 2) {
+        while (true) {
+          const int v = lane < NL ? vfull[slot * NL + lane] : s;
+          if (__builtin_amdgcn_ballot_w64(v < s) == 0ull) break;
+          __builtin_amdgcn_s_sleep(0);
+        }
+      }
+      if constexpr (MODE == 1) {
+        if (lane == 0) vfree[slot * NC + c] = s;
+        continue;
+      }
+      const uint8_t* sp = lds + slot * SL + lane * 16;
+      v4i b[FR];
+#pragma unroll
+      for (int f = 0; f < FR; ++f) b[f] = *reinterpret_cast<const v4i*>(sp + f * 1024);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (MODE != 2)
+        if (lane == 0) vfree[slot * NC + c] = s;
+#pragma unroll
+      for (int f = 0; f < FR; ++f)
+#pragma unroll
+        for (int i = 0; i < RF; ++i)
+          acc[i][f & 7] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[f], xa[i][f & 7], acc[i][f & 7], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < RF; ++i)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sum += acc[i][k][0] ^ acc[i][k][3];
+  }
+  __syncthreads();
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (sum == 0x1234567) sink[tid] = sum;
+  if (tid == 0) { out[blockIdx.x * 2] = t1 - t0; out[blockIdx.x * 2 + 1] = r1 - r0; }
+}
+
 typedef void (*KFn)(const int8_t*, int*, unsigned long long*);
 struct Var { const char* name; KFn f; int threads; int mode; };
 
-int main() {
+int main(int argc, char** argv) {
+  const bool pmc = argc > 1;                 // under rocprofv3 --pmc: 1 round, 3 launches each
   int ncu = 0;
   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
   const long wbytes = 2L * NCHUNK * SLOT;           // the 2 MB stream region (3 MB read per CU)
@@ -186,25 +307,34 @@ int main() {
     hipMemcpy(W, h, wbytes, hipMemcpyHostToDevice);
     free(h);
   }
+  // round 6: the round-5 best (8 waves, every wave DMAs + one s_barrier per slot) against
+  // dedicated loaders with FULL / FREE words (k_ring2 <NC consumers, NL loaders, slots,
+  // KB per slot, slots in flight>)
   Var vars[] = {
-      {"8w 4slot pd4 asm  dma global 64b ", k_ring<8, 4, true, false, 0, 4, true, true, 0, 0>, 512, 0},
-      {"8w 4slot pd4 asm  dma global saddr", k_ring<8, 4, true, false, 0, 4, true, true, 0, 1>, 512, 0},
-      {"8w consume-only pd4 asm           ", k_ring<8, 4, true, false, 2, 4, true, true>, 512, 2},
-      {"4w 4slot pd4 asm  dma global 64b  ", k_ring<4, 4, true, false, 0, 4, true, true, 0, 0>, 256, 0},
-      {"4w 4slot pd4 asm  dma global saddr", k_ring<4, 4, true, false, 0, 4, true, true, 0, 1>, 256, 0},
-      {"4w consume-only pd4 asm           ", k_ring<4, 4, true, false, 2, 4, true, true>, 256, 2},
-      {"4w fill-only global 64b           ", k_ring<4, 4, true, false, 1, 0, false, false, 0, 0>, 256, 1},
-      {"4w fill-only global saddr         ", k_ring<4, 4, true, false, 1, 0, false, false, 0, 1>, 256, 1},
+      {"r05 8w all-DMA+barrier 4x32K pd4  ", k_ring<8, 4, true, false, 0, 4, true, true, 0, 0>, 512, 0},
+      {"r05 8w consume-only pd4           ", k_ring<8, 4, true, false, 2, 4, true, true>, 512, 2},
+      {"r05 4w fill-only                  ", k_ring<4, 4, true, false, 1, 0, false, false, 0, 0>, 256, 1},
+      {"ring2 4c+4l 6x16K D2              ", k_ring2<4, 4, 6, 16, 2, 0, false>, 512, 0},
+      {"ring2 4c+4l 6x16K D2 nt           ", k_ring2<4, 4, 6, 16, 2, 0, true>, 512, 0},
+      {"ring2 4c+2l 6x16K D2              ", k_ring2<4, 2, 6, 16, 2, 0, false>, 384, 0},
+      {"ring2 4c+1l 6x16K D2              ", k_ring2<4, 1, 6, 16, 2, 0, false>, 320, 0},
+      {"ring2 4c+4l 8x16K D3              ", k_ring2<4, 4, 8, 16, 3, 0, false>, 512, 0},
+      {"ring2 4c+4l 5x16K D1              ", k_ring2<4, 4, 5, 16, 1, 0, false>, 512, 0},
+      {"ring2 4c+4l 4x32K D1              ", k_ring2<4, 4, 4, 32, 1, 0, false>, 512, 0},
+      {"ring2 8c+4l 6x16K D2              ", k_ring2<8, 4, 6, 16, 2, 0, false>, 768, 0},
+      {"ring2 4c+4l fill-only 6x16K D2    ", k_ring2<4, 4, 6, 16, 2, 1, false>, 512, 1},
+      {"ring2 4c consume-only 6x16K       ", k_ring2<4, 4, 6, 16, 2, 2, false>, 512, 2},
+      {"ring2 8c consume-only 6x16K       ", k_ring2<8, 4, 6, 16, 2, 2, false>, 768, 2},
   };
   printf("CUs %d; per CU %.2f MB streamed (96 x 32 KB slots); MFMA floor at 4 waves = 96 x 64 x 16 cycles\n",
          ncu, 3.0 * NCHUNK * SLOT / 1048576.0);
-  for (int rep = 0; rep < 2; ++rep)
+  for (int rep = 0; rep < (pmc ? 1 : 2); ++rep)
     for (const Var& v : vars) {
       auto launch = [&]() { v.f<<<ncu, v.threads>>>(W, sink, d); };
-      for (int w = 0; w < 3; ++w) launch();
+      for (int w = 0; w < (pmc ? 1 : 3); ++w) launch();
       hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
       hipEventRecord(e0);
-      const int reps = 20;
+      const int reps = pmc ? 2 : 20;
       for (int w = 0; w < reps; ++w) launch();
       hipEventRecord(e1); hipEventSynchronize(e1);
       float ms; hipEventElapsedTime(&ms, e0, e1);

@@ -27,6 +27,19 @@ def from_csv(path):
     return out
 
 
+def sources_sha16():
+    """Digest of the product kernel sources (onnx-transformer_amd/csrc/*.hip, *.h) the
+    profiled library was built from; bench.py compares it with the sources it runs."""
+    import hashlib
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "onnx-transformer_amd", "csrc")
+    h = hashlib.sha256()
+    for fn in sorted(glob.glob(os.path.join(root, "*.hip")) + glob.glob(os.path.join(root, "*.h"))):
+        with open(fn, "rb") as f:
+            h.update(os.path.basename(fn).encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def main(d):
     stats = sorted(glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True))
     if stats:
@@ -37,6 +50,7 @@ def main(d):
     rows.sort(key=lambda r: -r["total_ns"])
     tot = sum(r["total_ns"] for r in rows)
     print(f"source: `{os.path.relpath(src)}`  total kernel time {tot / 1e3:.1f} us\n")
+    print(f"kernel_sources_sha16: {sources_sha16()}\n")
     print("| kernel | calls | total us | avg us | min us | max us | % |")
     print("|---|---:|---:|---:|---:|---:|---:|")
     for r in rows:

@@ -73,7 +73,7 @@ def main():
     me = T(np.ones((Be, Se), np.uint8))
     ce = torch.empty((Be, Se, 512), device="cuda")
     cases = {
-        "attn_mfma cfg3": (lambda: L.qtx_attention_i8(P(qe), P(se), P(qe), P(se), P(qe), P(se), P(me), Se, 0, Be, 8, Se, Se, P(ce), S0), 8 * Be, 5),
+        "attn_mfma cfg3": (lambda: L.qtx_attention_i8(P(qe), P(se), P(qe), P(se), P(qe), P(se), P(me), Se, 0, Be, 8, Se, Se, P(ce), 0, S0), 8 * Be, 5),
         "dec_attn self": (lambda: L.qtx_decode_attention(1, P(y), 1536, P(kc), P(vc), P(skc), P(svc), 72, P(step), 0, S0, B, P(ctx), P(pma), S0), 8 * B, 5),
         "dec_attn cross": (lambda: L.qtx_decode_attention(0, P(y), 512, P(kc), P(vc), P(skc), P(svc), 72, S0, 72, P(mask), B, P(ctx), P(pma), S0), 8 * B, 5),
         "skinny I8 1536": (lambda: L.qtx_skinny_linear(0, P(a8), P(sa), S0, 512, S0, S0, S0, 0, P(W), P(sw), P(bias), B, 1536, 512, 8, 0, S0, P(out), S0, S0), 96 * B // 8, 4),
