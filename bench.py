@@ -437,6 +437,20 @@ def cpu_baseline(sd, B=32, S=72, max_len=72, seed=7):
     t0 = time.perf_counter()
     tp.encode(xe, me)
     t3 = time.perf_counter() - t0
+    # BASELINE.md §3's plan, torch.set_num_threads(os.cpu_count()): the same cfg2 decode on
+    # every CPU the host reports (on the GPU box the whole shared host, whose other GPUs'
+    # jobs use the same CPUs), beside the per-GPU share above (the value)
+    allc = os.cpu_count() or threads
+    allc_rate = None
+    if allc != threads:
+        torch.set_num_threads(allc)
+        try:
+            tp.greedy_decode(srct[:2], mask[:2], 4)
+            t0 = time.perf_counter()
+            tp.greedy_decode(srct, mask, max_len)
+            allc_rate = B * (max_len - 1) / (time.perf_counter() - t0)
+        finally:
+            torch.set_num_threads(threads)
     return {"value": B * (max_len - 1) / t2, "unit": "decoded tokens/s", "cores": int(threads),
             "kind": "port",
             "sample": f"oracle/torch_port.py (the reference's fp32 fake-quant arithmetic in "
@@ -445,6 +459,10 @@ def cpu_baseline(sd, B=32, S=72, max_len=72, seed=7):
                       f"host's CPU share per GPU; os.cpu_count()={os.cpu_count()} is the whole "
                       f"host, {affinity} CPUs in this process's affinity mask): cfg2 greedy "
                       f"decode B={B}, S={S}, {max_len - 1} steps in {t2:.1f}s",
+            "all_cpus": {"threads": int(allc), "value": allc_rate if allc_rate else B * (max_len - 1) / t2,
+                         "note": "cfg2 decode with torch.set_num_threads(os.cpu_count()) "
+                                 "(BASELINE.md §3's plan); the value above uses the host's "
+                                 "per-GPU CPU share (OMP_NUM_THREADS)"},
             "cfg1_b1_decode_tokens_per_s": (max_len - 1) / t1,
             "cfg3_encoder_s": t3,
             "cfg3_encoder_int8_ops_per_s": encoder_gemm_ops(256, 128) / t3}

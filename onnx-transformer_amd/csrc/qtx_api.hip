@@ -148,6 +148,8 @@ struct qtx_model {
   unsigned* status = nullptr;      // kStatusSlots 16-byte status words (model memory)
   std::mutex slot_mu;              // guards slot_used
   std::vector<bool> slot_used;     // a live thread holds the slot (qtx_api.hip CallStatus)
+  std::vector<bool> slot_had_owner;  // a thread held the slot before (its kernels may still
+                                     // be in flight on that thread's streams)
   // an exec may still be running on a caller's stream: wait for its last replay first
   void clear_graphs() {
     for (auto& kv : graphs) {
@@ -187,8 +189,10 @@ const char* status_text(unsigned v) {
 }
 // Status words live in the model's own memory: kStatusSlots 16-byte words, one per live
 // calling thread.  A thread's first model-level call that can raise a device error (the
-// encoder and greedy-decode entry points) claims a free slot and zeroes it on its stream;
-// the slot returns to the model when the thread exits.  A kernel that detects an error it
+// encoder and greedy-decode entry points) claims a free slot and zeroes it (call_status_begin);
+// the slot returns to the model when the thread exits.  A thread should check (or at least
+// synchronise) before it exits: an error its kernels raise after it is gone is dropped when
+// the next owner claims the slot.  A kernel that detects an error it
 // cannot repair (k_gemm_wsy's exchange timeout) ORs a DEV_E_* bit into the word, and the bit
 // stays until qtx_model_check reports it (later calls never clear it: ADVICE r04).
 // qtx_model_check(m, stream) synchronises the stream and reads the calling thread's word,
@@ -219,18 +223,32 @@ int status_slot_cap() {
   return n > 0 && n < kStatusSlots ? n : kStatusSlots;
 }
 
-// the calling thread's word for m (nullptr: every slot is held by a live thread); *fresh is
-// set when the slot was claimed by this call (its word must be zeroed)
-unsigned* thread_status_word(qtx_model* m, bool* fresh) {
-  *fresh = false;
+// the calling thread's word for m if it holds one (nullptr otherwise)
+unsigned* held_status_word(const qtx_model* m) {
   for (const CallStatus& c : t_calls.v)
     if (c.m == m && c.serial == m->serial) return m->status + 4 * c.slot;
+  return nullptr;
+}
+
+// the calling thread's word for m (nullptr: every slot is held by a live thread); *fresh is
+// set when the slot was claimed by this call (its word must be zeroed), *reused when a
+// thread held that slot before
+unsigned* thread_status_word(qtx_model* m, bool* fresh, bool* reused) {
+  *fresh = false;
+  *reused = false;
+  if (unsigned* w = held_status_word(m)) return w;
   int slot = -1;
   {
     std::lock_guard<std::mutex> lk(m->slot_mu);
     const int cap = status_slot_cap();
     for (int i = 0; i < cap; ++i)
-      if (!m->slot_used[i]) { m->slot_used[i] = true; slot = i; break; }
+      if (!m->slot_used[i]) {
+        m->slot_used[i] = true;
+        *reused = m->slot_had_owner[i];
+        m->slot_had_owner[i] = true;
+        slot = i;
+        break;
+      }
   }
   if (slot < 0) return nullptr;
   // drop the records of models destroyed since (their serials are gone from g_live)
@@ -258,18 +276,31 @@ void release_slot(const CallStatus& c) {
   m->slot_used[c.slot] = false;
 }
 
-// the calling thread's word (claimed and zeroed on st by its first call: a kernel,
-// graph-capturable and stream-ordered)
+// the calling thread's word, claimed and zeroed by its first status-carrying call on the
+// model: zeroed eagerly (a synchronous hipMemset, so a claim cannot be
+// captured into a graph and never run), and — when a thread held the slot before and may
+// have exited with kernels still in flight that can set a bit — after the device has
+// drained them, so no stale bit of the previous owner survives the zero
 int call_status_begin(const qtx_model* mc, unsigned** word, hipStream_t st) {
   qtx_model* m = const_cast<qtx_model*>(mc);
-  bool fresh = false;
-  *word = thread_status_word(m, &fresh);
+  if ((*word = held_status_word(m)) != nullptr) return QTX_OK;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIPCHK(hipStreamIsCapturing(st, &cs));
+  if (cs != hipStreamCaptureStatusNone)
+    return fail(QTX_E_INVALID,
+                "a thread's first encoder / greedy call on a model claims its device status "
+                "word and cannot be stream-captured: make one uncaptured call first");
+  bool fresh = false, reused = false;
+  *word = thread_status_word(m, &fresh, &reused);
   if (!*word)
     return fail(QTX_E_UNSUPPORTED,
                 "every device status word of this model is held by a live thread (%d): "
                 "at most that many threads may call one model at a time",
                 status_slot_cap());
-  if (fresh) HIPCHK(launch_zero(*word, 16, st));
+  if (fresh) {
+    if (reused) HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemset(*word, 0, 16));
+  }
   return QTX_OK;
 }
 
@@ -368,8 +399,13 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
         for (QLin* L : {&e.qkv, &e.w1}) L->qws32 = ar.take<int8_t>((size_t)L->N * L->K);
 #endif
       }
-    if (c.d_ff % 64 == 0)    // the fused FFN's weight stream (F KB per layer)
+#ifdef QTX_DIAG
+    // the fused FFN's weight stream (F KB per layer): only where QTX_FFN_FUSED_MIN_M can turn
+    // that launch on (the diagnostic build; measured slower than the split launches, DESIGN
+    // §4), not 12 MB of every product model
+    if (c.d_ff % 64 == 0)
       for (auto& e : m->enc) e.ffn = ar.take<int8_t>((size_t)F * 1024);
+#endif
     lin(m->ckv_all, NL * 2 * D, D);
     for (int l = 0; l < NL; ++l) {   // dec[l].ckv: rows 2Dl .. 2D(l+1) of ckv_all
       QLin& v = m->dec[l].ckv;
@@ -401,6 +437,7 @@ int32_t qtx_model_create(const qtx_config* cfg, const float* const* t, int32_t n
   static std::atomic<unsigned long long> next_serial{1};
   m->serial = next_serial.fetch_add(1);
   m->slot_used.assign(kStatusSlots, false);
+  m->slot_had_owner.assign(kStatusSlots, false);
   {
     std::lock_guard<std::mutex> lk(g_live_mu);
     g_live[m->serial] = m;

@@ -467,6 +467,9 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
     // (in-order within the wave, conflict-free) lane l takes row l >> 4 of column l & 15 —
     // one output per lane instead of four on a quarter of the lanes
     if (fg == 0) tail[wave][fr] = acc;
+    // (no instruction: keeps the compiler from moving the other lanes' reads above the
+    // store — the hardware keeps one wave's LDS operations in order)
+    __builtin_amdgcn_wave_barrier();
     const int v = reinterpret_cast<const int*>(&tail[wave][fr])[fg];
     const int row = m0 + fg;
     const bool ok = cok && row < g.M;
@@ -490,6 +493,7 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
     // remap, lane l takes rows (l >> 4) and (l >> 4) + 4 of column l & 15 — two outputs per
     // lane instead of four on half of the lanes
     if (fg < RPL) tail[wave][16 * fg + fr] = acc;
+    __builtin_amdgcn_wave_barrier();      // as at RB == 4
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
       const int v = reinterpret_cast<const int*>(&tail[wave][16 * j + fr])[fg];

@@ -39,10 +39,6 @@ struct Knobs {
   long ws_min_m = 2048;      // QTX_WS_MIN_M: weight-stationary from this many rows
   long ws_res_min_m = 2048;  // QTX_WS_RES_MIN_M / _MAX_M: the O-projection's WS range
   long ws_res_max_m = 8192;
-  bool no_ffn_fused = false; // QTX_NO_FFN_FUSED: the encoder FFN as FFN1 + FFN2 launches
-  // QTX_FFN_FUSED_MIN_M: the fused FFN launch from this many rows (default: off — measured
-  // slower than the split launches at cfg3, DESIGN.md §4 "The fused FFN kernel")
-  long ffn_fused_min_m = 1L << 40;
   int status_slots = 0;      // QTX_STATUS_SLOTS: device status words per model (0: all 256;
                              // tests lower it to make exhaustion happen)
   // ---- hooks of the FFN1 exchange's error path (tests/test_gpu_status.py)
@@ -63,6 +59,12 @@ struct Knobs {
                                         // the device counter even where the host knows it
   QTX_DKNOB(bool, int4_packed, false);  // QTX_INT4_PACKED: a 4-bit model's decode step on the
                                         // packed int4 kernels
+  // QTX_FFN_FUSED_MIN_M: the encoder's fused FFN launch (k_ffn_fused) from this many rows
+  // (default off — measured slower than the split launches at cfg3, DESIGN.md §4 "The fused
+  // FFN kernel"; the product keeps it as the C-ABI entry qtx_ffn_rows only);
+  // QTX_NO_FFN_FUSED: never
+  QTX_DKNOB(long, ffn_fused_min_m, 1L << 40);
+  QTX_DKNOB(bool, no_ffn_fused, false);
   int ablate = 0;            // QTX_ABLATE: kernel classes dropped from the decode step
   bool ablate_nop = false;   // QTX_ABLATE_NOP
   bool dbg_tail = false;     // QTX_DBG_TAIL

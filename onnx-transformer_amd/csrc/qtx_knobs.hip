@@ -38,8 +38,6 @@ Knobs read_env() {
   k.ws_res_min_m = num("QTX_WS_RES_MIN_M", 2048L);
   k.ws_res_max_m = num("QTX_WS_RES_MAX_M", 8192L);
   k.status_slots = (int)num("QTX_STATUS_SLOTS", 0);
-  k.no_ffn_fused = flag("QTX_NO_FFN_FUSED");
-  k.ffn_fused_min_m = num("QTX_FFN_FUSED_MIN_M", 1L << 40);
   k.wsx_spin_limit = (int)num("QTX_WSX_SPIN_LIMIT", -1);
   k.wsx_drop_slice = (int)num("QTX_WSX_DROP_SLICE", -1);
 #ifdef QTX_DIAG
@@ -52,6 +50,8 @@ Knobs read_env() {
   k.hquant_rows = flag("QTX_HQUANT_ROWS");
   k.device_step = flag("QTX_DEVICE_STEP");
   k.int4_packed = flag("QTX_INT4_PACKED");
+  k.no_ffn_fused = flag("QTX_NO_FFN_FUSED");
+  k.ffn_fused_min_m = num("QTX_FFN_FUSED_MIN_M", 1L << 40);
   k.ablate = (int)num("QTX_ABLATE", 0);
   k.ablate_nop = flag("QTX_ABLATE_NOP");
   k.dbg_tail = flag("QTX_DBG_TAIL");

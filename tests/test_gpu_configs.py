@@ -66,10 +66,11 @@ def cfg3_split(torch, gpu_model, cfg3_inputs):
     return _encode(torch, gpu_model, x, m)
 
 
-@pytest.mark.parametrize("env", [{"QTX_FFN_FUSED_MIN_M": 1}, {"QTX_NO_WSX": 1}])
+@pytest.mark.parametrize("env", [pytest.param({"QTX_FFN_FUSED_MIN_M": 1}, marks=pytest.mark.diag),
+                                 {"QTX_NO_WSX": 1}])
 def test_cfg3_encoder_ffn_paths_agree(torch, gpu_model, cfg3_inputs, cfg3_split, knob_env, env):
     """The default encoder (the one-pass FFN1 with the in-launch exchange + the FFN2 row
-    GEMM) against the fused FFN launch (k_ffn_fused, QTX_FFN_FUSED_MIN_M) and the two-pass
+    GEMM) against the fused FFN launch (k_ffn_fused, QTX_FFN_FUSED_MIN_M: diagnostic build) and the two-pass
     FFN1 (QTX_NO_WSX), which also runs the batch as two half-batch streams — the same bits."""
     x, m = cfg3_inputs
     for k, v in env.items():
@@ -95,7 +96,7 @@ def test_cfg3_encoder_sample_matches_oracle(torch, oracle_model, cfg3_inputs, cf
     np.testing.assert_array_equal(cfg3_split[b:b + 1], oracle_model.encode(x[b:b + 1], m[b:b + 1]))
 
 
-@pytest.mark.parametrize("env", [{}, {"QTX_FFN_FUSED_MIN_M": 1}])
+@pytest.mark.parametrize("env", [{}, pytest.param({"QTX_FFN_FUSED_MIN_M": 1}, marks=pytest.mark.diag)])
 def test_cfg3_encoder_split_two_threads(torch, gpu_model, cfg3_inputs, cfg3_split, knob_env, env):
     """Two threads share the model handle, each on its own stream with its own inputs, at
     the same time, with the one-pass FFN1 whose workgroups wait for their partner slices

@@ -264,3 +264,43 @@ def test_status_slots_exhaustion_is_loud(torch, state_dict, knob_env):
         t.start()
         t.join(timeout=60)
     assert res == {f"s{i}": "ok" for i in range(12)}, res
+
+
+def test_reclaimed_slot_drops_stale_error(torch, state_dict, knob_env):
+    """a thread that exits with its encode still in flight and a device error
+    unreported (its FFN1 exchange times out after it is gone) returns its status word to
+    the model; the next thread to claim that word (the cap lowered to 1, so it must be the
+    same word) starts clean — the claim drains the device before zeroing the word — and its
+    own clean encode checks clean."""
+    import threading
+    from qtx.model import QtxModel
+    knob_env("QTX_STATUS_SLOTS", 1)
+    knob_env("QTX_NO_FFN_FUSED", 1)                    # FFN1 on the one-pass exchange
+    model = QtxModel(state_dict)
+    x, mk = _cfg3(torch)
+    torch.cuda.synchronize()
+    knob_env("QTX_WSX_SPIN_LIMIT", 64)
+    knob_env("QTX_WSX_DROP_SLICE", 2)
+    res = {}
+
+    def leaver():
+        with torch.cuda.stream(torch.cuda.Stream()):
+            model.encode(x, mk)                        # times out on the device; no check
+        res["a"] = "left"
+    a = threading.Thread(target=leaver)
+    a.start()
+    a.join(timeout=60)
+    knob_env("QTX_WSX_DROP_SLICE", -1)
+
+    def claimer():
+        try:
+            with torch.cuda.stream(torch.cuda.Stream()):
+                model.encode(x, mk)
+                model.check()
+            res["b"] = "clean"
+        except Exception as e:             # noqa: BLE001 - reported below
+            res["b"] = repr(e)
+    b = threading.Thread(target=claimer)
+    b.start()
+    b.join(timeout=60)
+    assert res == {"a": "left", "b": "clean"}, res
