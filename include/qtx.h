@@ -352,7 +352,9 @@ int32_t qtx_skinny_linear(int32_t amode, const int8_t* A, const float* sa, const
  *   per token, k/v written to the caches at row b*kv_bs + *step_dev, keys 0..*step_dev
  *   (kv_bs <= 128).
  * kv_new = 0 (cross): y [B,512] holds q; keys = S cached rows per sentence, mask [B,S].
- * Caches: kc/vc int8 [B][kv_bs][512], skc/svc [B][kv_bs].  Out: fp32 context ctx [B,512]
+ * Caches: kc int8 [B][kv_bs][512]; vc int8 in groups of 4 keys, [B][ceil(kv_bs/4)][512][4]
+ *   (byte ((b*G4 + j/4)*512 + d)*4 + j%4 holds v[b][j][d]: one dword = 4 keys of one dim);
+ *   skc/svc [B][kv_bs].  Out: fp32 context ctx [B,512]
  * and the per-head absmax pmax [8][B] (the next GEMM's per-token quantization, amode 2 of
  * qtx_skinny_linear with pmax_n = 8).  Keys <= 128.  The PV MatMul runs in the decoder's
  * canonical order (four partial chains; qtx_attention_i8 with dec = 1). */

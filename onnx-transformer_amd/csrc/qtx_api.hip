@@ -1201,7 +1201,9 @@ size_t dec_ws(const qtx_config& c, int B, int T, int S) {
 struct GreedyWS {
   Scratch enc, dec;
   CrossKV cross;
-  std::vector<int8_t*> kc, vc;
+  std::vector<int8_t*> cvg;   // the cross values in k_dec_attn's 4-key groups, per layer
+  std::vector<int8_t*> kc, vc;   // self K [B][max_len][D]; V in 4-key groups (fused step) or
+                                 // [B][max_len][D] (unfused step)
   std::vector<float*> skc, svc;
   float* memory;
   float* xo;
@@ -1242,10 +1244,13 @@ GreedyWS carve_greedy(Arena& ar, const qtx_config& c, int B, int S, int max_len)
   g.enc = carve_scratch(ar, c, (long)B * S);
   g.dec = carve_scratch(ar, c, B);
   g.cross = carve_cross(ar, c, (long)B * S);
+  // the cross values regrouped once per decode (layer stride: B * ceil(S/4) * 4 * D bytes)
+  int8_t* cvg = ar.take<int8_t>((size_t)c.n_layers * B * ((S + 3) & ~3) * D);
   for (int l = 0; l < c.n_layers; ++l) {
+    g.cvg.push_back(cvg ? cvg + (size_t)l * B * ((S + 3) & ~3) * D : nullptr);
     g.kc.push_back(ar.take<int8_t>((size_t)B * max_len * D));
     g.skc.push_back(ar.take<float>((size_t)B * max_len));
-    g.vc.push_back(ar.take<int8_t>((size_t)B * max_len * D));
+    g.vc.push_back(ar.take<int8_t>((size_t)B * ((max_len + 3) & ~3) * D));
     g.svc.push_back(ar.take<float>((size_t)B * max_len));
   }
   g.memory = ar.take<float>((size_t)B * S * D);
@@ -1270,9 +1275,10 @@ GreedyWS group_view(const GreedyWS& g, const qtx_config& c, int i, int b0, int S
   GreedyWS v = g;
   v.dec = g.grp[i];
   for (int l = 0; l < c.n_layers; ++l) {
-    v.kc[l] += b0 * max_len * D; v.vc[l] += b0 * max_len * D;
+    v.kc[l] += b0 * max_len * D; v.vc[l] += b0 * ((max_len + 3) & ~3) * D;
     v.skc[l] += b0 * max_len; v.svc[l] += b0 * max_len;
     v.cross.k8[l] += b0 * S * D; v.cross.v8[l] += b0 * S * D;
+    v.cvg[l] += b0 * ((S + 3) & ~3) * D;
     v.cross.sk[l] += b0 * S; v.cross.sv[l] += b0 * S;
   }
   v.logits += (long)b0 * c.tgt_vocab;
@@ -1374,7 +1380,7 @@ int greedy_step_fused(const qtx_model* m, GreedyWS& g, int B, int S, int max_len
     RC(ln_linear(L.cq, L.ln[1], 0, s.y, D, 2));
     at = DecAttnArgs{};
     at.y = s.y; at.ldy = D; at.kv_new = 0; at.S = S; at.mask = src_mask;
-    at.kc = g.cross.k8[l]; at.vc = g.cross.v8[l]; at.skc = g.cross.sk[l];
+    at.kc = g.cross.k8[l]; at.vc = g.cvg[l]; at.skc = g.cross.sk[l];
     at.svc = g.cross.sv[l]; at.kv_bs = S;
     at.ctx = s.ctx; at.pmax = own_max ? nullptr : g.pmax_a; at.B = B;
     QTX_RUN(8, launch_dec_attn(at, B, st));
@@ -1716,6 +1722,11 @@ int greedy_run(const qtx_model* m, GreedyWS& g, const int64_t* src, int B, int S
                       g.enc.x, (long)S * D, st));
   RC(encoder_run(m, g.enc.x, src_mask, B, S, g.memory, g.enc, st, f));
   RC(cross_kv(m, g.memory, B * S, g.cross, st));
+  if (fused) {   // the cross values of every layer in k_dec_attn's 4-key groups
+    const long v_ls = g.cross.v8.size() > 1 ? (long)(g.cross.v8[1] - g.cross.v8[0]) : 0;
+    HIPCHK(launch_vgroup4(g.cross.v8[0], v_ls, c.n_layers, B, S, g.cvg[0],
+                          (long)B * ((S + 3) & ~3) * D, st));
+  }
 
   // ids[:, 0] = start ; step[0] = position 0, step[1] = arrival counter
   HIPCHK(launch_fill_col(ids, max_len, B, start, st));

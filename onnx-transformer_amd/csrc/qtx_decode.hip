@@ -663,12 +663,19 @@ hipError_t launch_skinny(const SkinnyArgs& g, int wbits, hipStream_t st) {
 // the output-projection GEMM (A_F32Q), so no cross-workgroup step is needed here.
 // Keys staged in LDS (<= 128).  Grid (B, 8): the 8 heads of sentence b share blockIdx.x,
 // so with B % 8 == 0 they land on one XCD (workgroups go round-robin over the 8 XCDs).
+// The value cache is kept in groups of 4 keys (round 6): byte ((b * G4 + j / 4) * 512 + d) * 4
+// + j % 4 holds v[b][j][d] (G4 = ceil(kv_bs / 4)), so one dword is 4 consecutive keys of one
+// dim — the PV's 4-key step in one ds_read_b32 and 4 SDWA conversions instead of 4 byte
+// reads.  Key rows are staged 20 dwords apart (16 B aligned: ds_read_b128 / ds_write_b128,
+// conflict-free: 20 j mod 64 steps through distinct 4-bank groups over 16 lanes).
 // =====================================================================================
 constexpr int DEC_MAXK = 128;
+constexpr int DEC_KST = 20;   // staged key row stride in dwords
 
 template <bool KV_NEW, int NIT>
 __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
-  __shared__ uint32_t Ks[DEC_MAXK * 17];   // key rows of this head: 16 dwords (+1 pad)
+  __shared__ __attribute__((aligned(16))) uint32_t Ks[DEC_MAXK * DEC_KST];   // key rows of this head
+  // values of this head, 4-key groups: dword g * 64 + d = keys 4g .. 4g + 3 of dim d
   __shared__ __attribute__((aligned(16))) uint8_t Vs[DEC_MAXK * 64];
   __shared__ float svs[DEC_MAXK];
   __shared__ __attribute__((aligned(16))) float PS[DEC_MAXK];   // RN(P_j * s_v[j]), 0 past Sk
@@ -679,6 +686,7 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   // rows staged (self: rows 0 .. the position when the host passes it, else all allocated)
   const int nrows = KV_NEW ? (a.host_step1 > 0 ? a.host_step1 : (int)a.kv_bs) : a.S;
   const long kvb = (long)b * a.kv_bs;
+  const long vgb = (long)b * ((a.kv_bs + 3) >> 2);     // the sentence's first value group
 
   // phase 0: every global load first (one memory latency): this step's q (k, v) rows
   // first — vmcnt retires in issue order, so their quantization (phase 1) then runs while
@@ -699,20 +707,19 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   // clamped: a stale position (a counter not reset) must not index past the cache
   const int step = !KV_NEW ? 0 : a.host_step1 > 0 ? a.host_step1 - 1 : min(max(*a.step, 0), (int)a.kv_bs - 1);
   const int rsub = lane >> 2, ch = lane & 3;
+  // values: per 16 keys, 4 groups x this head's 64 dims x 4 B = 1 KB, lane = group
+  // 4 i + lane / 16, dims 4 (lane % 16) .. + 3
+  const int vg = lane >> 4, vd = 4 * (lane & 15), glast = (nrows - 1) >> 2;
   uint4 kr[NIT], vr[NIT];
 #pragma unroll
   for (int i = 0; i < NIT; ++i) {
     const int r = min(16 * i + rsub, nrows - 1);
     const long off = (kvb + r) * 512 + h * 64 + 16 * ch;
-#ifdef QTX_KV_DEFAULT_POLICY   // experiment: default cache policy on the K/V rows
-    kr[i] = *reinterpret_cast<const uint4*>(a.kc + off);
-    vr[i] = *reinterpret_cast<const uint4*>(a.vc + off);
-#else
+    const long voff = ((vgb + min(4 * i + vg, glast)) * 512 + h * 64 + vd) * 4;
     // non-temporal: each K/V row is read once per step by one wave, so it should not push
     // the weights (re-read every step) out of the XCD's L2 (B = 256: 36.2 -> 35.1 ms)
     kr[i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(a.kc + off)));
-    vr[i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(a.vc + off)));
-#endif
+    vr[i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(a.vc + voff)));
   }
   const int j0 = min(lane, nrows - 1), j1 = min(lane + 64, nrows - 1);
   float sk0 = a.skc[kvb + j0], sk1 = a.skc[kvb + j1];
@@ -751,7 +758,7 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
     vq = (int8_t)quant_one(v_own, sv);
     const long row = kvb + step;
     a.kc[row * 512 + h * 64 + lane] = kq;     // cache append (attention.py: k/v of this step)
-    a.vc[row * 512 + h * 64 + lane] = vq;
+    a.vc[((vgb + (step >> 2)) * 512 + h * 64 + lane) * 4 + (step & 3)] = vq;
     if (h == 0 && lane == 0) { a.skc[row] = sk; a.svc[row] = sv; }
   }
 
@@ -759,15 +766,14 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
 #pragma unroll
   for (int i = 0; i < NIT; ++i) {
     const int r = min(16 * i + rsub, nrows - 1);
-    uint32_t* kd = &Ks[r * 17 + 4 * ch];
-    kd[0] = kr[i].x; kd[1] = kr[i].y; kd[2] = kr[i].z; kd[3] = kr[i].w;
-    *reinterpret_cast<uint4*>(Vs + r * 64 + 16 * ch) = vr[i];
+    *reinterpret_cast<uint4*>(&Ks[r * DEC_KST + 4 * ch]) = kr[i];
+    *reinterpret_cast<uint4*>(Vs + (min(4 * i + vg, glast) * 64 + vd) * 4) = vr[i];
   }
   svs[j0] = sv0; svs[j1] = sv1;
   __syncthreads();
   if constexpr (KV_NEW) {
-    reinterpret_cast<int8_t*>(&Ks[step * 17])[lane] = kq;
-    Vs[step * 64 + lane] = (uint8_t)vq;
+    reinterpret_cast<int8_t*>(&Ks[step * DEC_KST])[lane] = kq;
+    Vs[((step >> 2) * 64 + lane) * 4 + (step & 3)] = (uint8_t)vq;
     if (lane == 0) svs[step] = sv;
     if (lane == step) sk0 = sk;            // the key scales stay in the lane that scores
     if (lane + 64 == step) sk1 = sk;       // the key (lane + 64 u)
@@ -786,9 +792,20 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   for (int u = 0; u < 2; ++u) {
     const int j = lane + 64 * u;
     if (j < Sk) {
-      int acc = 0;
+      // the key row in 4 ds_read_b128; two partial int32 sums (exact in any order)
+      uint32_t kw[16];
 #pragma unroll
-      for (int w = 0; w < 16; ++w) acc = __builtin_amdgcn_sdot4(qd[w], Ks[j * 17 + w], acc, false);
+      for (int w4 = 0; w4 < 4; ++w4) {
+        const uint4 t = *reinterpret_cast<const uint4*>(&Ks[j * DEC_KST + 4 * w4]);
+        kw[4 * w4] = t.x; kw[4 * w4 + 1] = t.y; kw[4 * w4 + 2] = t.z; kw[4 * w4 + 3] = t.w;
+      }
+      int a0 = 0, a1 = 0;
+#pragma unroll
+      for (int w = 0; w < 16; w += 2) {
+        a0 = __builtin_amdgcn_sdot4(qd[w], kw[w], a0, false);
+        a1 = __builtin_amdgcn_sdot4(qd[w + 1], kw[w + 1], a1, false);
+      }
+      const int acc = a0 + a1;
       float s = (((float)acc * sq) * (u ? sk1 : sk0)) * 0.125f;
       if (!(u ? keep1 : keep0)) s = -1.0e9f;
       sc[u] = s;
@@ -828,8 +845,10 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   // summed (c0 + c1) + (c2 + c3).  Per 16-key group the four chains' fmas are independent,
   // so the lone wave's dependent chain is a quarter of the keys (it was one fma per key,
   // 26-46 cycles each).  Padded keys: PS == 0 and a finite v, fma(0, v, acc) == acc.
+  // The values of 4 keys of the lane's dim in one dword (the 4-key group layout): one
+  // ds_read_b32 per chain step of 4 keys, each byte converted by one SDWA v_cvt_f32_i32.
   float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
-  const int8_t* vl = reinterpret_cast<const int8_t*>(Vs) + lane;
+  const uint32_t* vl = reinterpret_cast<const uint32_t*>(Vs) + lane;
 #pragma unroll 2
   for (int g = 0; g < nk16; g += 16) {
     const float4 p0 = *reinterpret_cast<const float4*>(PS + g);
@@ -838,11 +857,20 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
     const float4 p3 = *reinterpret_cast<const float4*>(PS + g + 12);
     float v[16];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) v[e] = (float)vl[(g + e) * 64];
-    c0 = fmaf(p0.x, v[0], c0);  c1 = fmaf(p1.x, v[4], c1);  c2 = fmaf(p2.x, v[8], c2);  c3 = fmaf(p3.x, v[12], c3);
-    c0 = fmaf(p0.y, v[1], c0);  c1 = fmaf(p1.y, v[5], c1);  c2 = fmaf(p2.y, v[9], c2);  c3 = fmaf(p3.y, v[13], c3);
-    c0 = fmaf(p0.z, v[2], c0);  c1 = fmaf(p1.z, v[6], c1);  c2 = fmaf(p2.z, v[10], c2); c3 = fmaf(p3.z, v[14], c3);
-    c0 = fmaf(p0.w, v[3], c0);  c1 = fmaf(p1.w, v[7], c1);  c2 = fmaf(p2.w, v[11], c2); c3 = fmaf(p3.w, v[15], c3);
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t d = vl[(g / 4 + q) * 64];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * q + e] = (float)(int8_t)(d >> (8 * e));
+    }
+    // each fma an asm v_fmac_f32 (the IEEE fused multiply-add, as fmaf): left to itself the
+    // compiler SLP-packs the four chains into v_pk_fma_f32 pairs — no faster on gfx950 (a
+    // packed fp32 op issues at half rate) — and assembles their operand pairs with ~1 v_mov
+    // per fma
+    auto fmac = [](float& c, float p, float x) { asm("v_fmac_f32 %0, %1, %2" : "+v"(c) : "v"(p), "v"(x)); };
+    fmac(c0, p0.x, v[0]);  fmac(c1, p1.x, v[4]);  fmac(c2, p2.x, v[8]);  fmac(c3, p3.x, v[12]);
+    fmac(c0, p0.y, v[1]);  fmac(c1, p1.y, v[5]);  fmac(c2, p2.y, v[9]);  fmac(c3, p3.y, v[13]);
+    fmac(c0, p0.z, v[2]);  fmac(c1, p1.z, v[6]);  fmac(c2, p2.z, v[10]); fmac(c3, p3.z, v[14]);
+    fmac(c0, p0.w, v[3]);  fmac(c1, p1.w, v[7]);  fmac(c2, p2.w, v[11]); fmac(c3, p3.w, v[15]);
   }
   const float acc = (c0 + c1) + (c2 + c3);
   QTX_STAMP(3);
@@ -885,6 +913,36 @@ hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st) {
   }
   if (a.S <= 0 || a.S > DEC_MAXK) return hipErrorInvalidValue;
   return dec_attn_nit<false>(a, B, a.S, st);
+}
+
+// k_vgroup4: a [B * S, 512] int8 value matrix (L layers, layer stride v_ls) into k_dec_attn's
+// 4-key group layout (byte ((b * G4 + g) * 512 + d) * 4 + e = v[b * S + 4 g + e][d], 0 past
+// S; G4 = ceil(S / 4); layer stride o_ls): the decode's cross values, once per decode.
+__global__ void k_vgroup4(const int8_t* v, long v_ls, int B, int S, int8_t* out, long o_ls) {
+  const int G4 = (S + 3) >> 2;
+  const long n = (long)B * G4 * 512;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int d = (int)(i & 511);
+  const long bg = i >> 9;
+  const int g = (int)(bg % G4), b = (int)(bg / G4);
+  const int8_t* src = v + (long)blockIdx.y * v_ls;
+  uint32_t w = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int j = 4 * g + e;
+    const uint32_t byte = j < S ? (uint8_t)src[((long)b * S + j) * 512 + d] : 0u;
+    w |= byte << (8 * e);
+  }
+  reinterpret_cast<uint32_t*>(out + (long)blockIdx.y * o_ls)[i] = w;
+}
+
+hipError_t launch_vgroup4(const int8_t* v, long v_ls, int L, int B, int S, int8_t* out,
+                          long o_ls, hipStream_t st) {
+  if (B <= 0 || S <= 0 || L <= 0) return hipSuccess;
+  const long n = (long)B * ((S + 3) / 4) * 512;
+  k_vgroup4<<<dim3((unsigned)((n + 255) / 256), L), dim3(256), 0, st>>>(v, v_ls, B, S, out, o_ls);
+  return hipGetLastError();
 }
 
 // =====================================================================================

@@ -56,6 +56,8 @@ struct SkinnyArgs {
 //                        masked by mask[b*S + j].
 //   Both write the fp32 context ctx [B, 512] and the per-head partial absmax
 //   pmax [8][B]; the next GEMM quantizes the row per token from them (A_F32Q).
+//   Caches: kc [B][kv_bs][512]; vc in groups of 4 keys, [B][ceil(kv_bs / 4)][512][4]
+//   (byte ((b * G4 + j / 4) * 512 + d) * 4 + j % 4 = v[b][j][d]; launch_vgroup4).
 struct DecAttnArgs {
   const float* y; long ldy;
   int8_t* kc; int8_t* vc; float* skc; float* svc; long kv_bs;   // [B][kv_bs rows][512]
@@ -213,6 +215,10 @@ hipError_t launch_pack_ffn(const int8_t* W1, const int8_t* W2, int F, int8_t* ou
 hipError_t launch_gemm(const GemmArgs& a, int wbits, hipStream_t st);
 hipError_t launch_skinny(const SkinnyArgs& a, int wbits, hipStream_t st);
 hipError_t launch_dec_attn(const DecAttnArgs& a, int B, hipStream_t st);
+// [B * S, 512] int8 values (L layers, layer stride v_ls) -> k_dec_attn's 4-key group layout
+// (DecAttnArgs::vc; layer stride o_ls, B * ceil(S / 4) * 2048 bytes per layer)
+hipError_t launch_vgroup4(const int8_t* v, long v_ls, int L, int B, int S, int8_t* out,
+                          long o_ls, hipStream_t st);
 // per-token int8 quantization of fp32 rows of 2048 (q row-major [M, 2048], s [M])
 hipError_t launch_quant_h2048(const float* X, long ldx, int M, int8_t* q, float* s,
                               hipStream_t st);

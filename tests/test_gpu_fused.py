@@ -156,8 +156,23 @@ def test_skinny_own_max_prologue(torch, M, K):
                                   res + O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b))
 
 
+def vgroup4(v):
+    """[B, n, 512] int8 values -> qtx_decode_attention's 4-key group layout
+    [B, ceil(n/4), 512, 4] (include/qtx.h)."""
+    B, n, D = v.shape
+    g4 = (n + 3) // 4
+    vp = np.zeros((B, 4 * g4, D), np.int8)
+    vp[:, :n] = v
+    return np.ascontiguousarray(vp.reshape(B, g4, 4, D).transpose(0, 1, 3, 2))
+
+
+def vungroup4(vg, n):
+    B, g4, D, _ = vg.shape
+    return vg.transpose(0, 1, 3, 2).reshape(B, 4 * g4, D)[:, :n]
+
+
 @pytest.mark.parametrize("B,step,kv_bs", [(2, 0, 8), (3, 5, 8), (32, 40, 72), (1, 127, 128),
-                                          (4, 70, 72), (2, 15, 17)])
+                                          (4, 70, 72), (2, 15, 17), (2, 16, 17)])
 def test_decode_self_attention(torch, B, step, kv_bs):
     rng = np.random.default_rng(B * 1000 + step)
     y = rng.standard_normal((B, 1536)).astype(f32)
@@ -165,7 +180,7 @@ def test_decode_self_attention(torch, B, step, kv_bs):
     vc = rng.integers(-127, 128, (B, kv_bs, 512)).astype(np.int8)
     skc = rng.uniform(0.002, 0.03, (B, kv_bs)).astype(f32)
     svc = rng.uniform(0.002, 0.03, (B, kv_bs)).astype(f32)
-    kcd, vcd, skd, svd = dev(torch, kc), dev(torch, vc), dev(torch, skc), dev(torch, svc)
+    kcd, vcd, skd, svd = dev(torch, kc), dev(torch, vgroup4(vc)), dev(torch, skc), dev(torch, svc)
     stepd = dev(torch, np.array([step], np.int32))
     ctxd = torch.empty((B, 512), dtype=torch.float32, device="cuda")
     pm = torch.empty((8, B), dtype=torch.float32, device="cuda")
@@ -177,7 +192,7 @@ def test_decode_self_attention(torch, B, step, kv_bs):
     qv, sv = O.quant_rows(y[:, 1024:])
     kc[:, step], vc[:, step], skc[:, step], svc[:, step] = qk, qv, sk, sv
     np.testing.assert_array_equal(kcd.cpu().numpy(), kc)       # cache append
-    np.testing.assert_array_equal(vcd.cpu().numpy(), vc)
+    np.testing.assert_array_equal(vungroup4(vcd.cpu().numpy(), kv_bs), vc)
     np.testing.assert_array_equal(skd.cpu().numpy(), skc)
     n = step + 1
     ctx, _ = O.attention(qq[:, None], sq[:, None], kc[:, :n], skc[:, :n], vc[:, :n],
@@ -206,7 +221,7 @@ def test_decode_cross_attention(torch, B, S, holes):
         mask[2, 70] = 1
     ctxd = torch.empty((B, 512), dtype=torch.float32, device="cuda")
     pm = torch.empty((8, B), dtype=torch.float32, device="cuda")
-    call("qtx_decode_attention", 0, P(dev(torch, y)), 512, P(dev(torch, kc)), P(dev(torch, vc)),
+    call("qtx_decode_attention", 0, P(dev(torch, y)), 512, P(dev(torch, kc)), P(dev(torch, vgroup4(vc))),
          P(dev(torch, skc)), P(dev(torch, svc)), S, S0, S, P(dev(torch, mask)), B, P(ctxd),
          P(pm), S0)
     qq, sq = O.quant_rows(y)

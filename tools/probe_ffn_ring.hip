@@ -28,8 +28,12 @@ constexpr int NCHUNK = 32;                 // 64-column FFN1 mini-chunks (d_ff 2
 constexpr int NSTREAM = 3 * NCHUNK;        // slots consumed per block
 
 // DMA issue forms: 0 global_load_lds 64-bit VGPR address; 1 global_load_lds SGPR base +
-// 32-bit VGPR offset (a buffer_load ... lds with ADD_TID_ENABLE, no VGPR operand at all,
-// faulted on the GPU as first written: not kept)
+// 32-bit VGPR offset.  A third form — buffer_load_dwordx4 ... lds with ADD_TID_ENABLE in the
+// V# (no VGPR address operand: lane i's 16 bytes at base + soffset + i * stride) — failed its
+// data check and lost the context in round 5 (never committed) and again, re-derived from
+// the MUBUF rules, in round 6 (stride 16, num_records in records, DATA_FORMAT 32; encoding
+// "buffer_load_dwordx4 off, s[0:3], sN lds" with M0 = the LDS slot): dropped for good,
+// DESIGN.md §4 and profiles/r06_ring_probe.log.
 template <int DM>
 __device__ __forceinline__ void dmax(const int8_t* base, unsigned off, unsigned voff, const uint8_t* lds_dst) {
   const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
@@ -315,19 +319,23 @@ int main(int argc, char** argv) {
       {"r05 8w consume-only pd4           ", k_ring<8, 4, true, false, 2, 4, true, true>, 512, 2},
       {"r05 4w fill-only                  ", k_ring<4, 4, true, false, 1, 0, false, false, 0, 0>, 256, 1},
       {"ring2 4c+4l 6x16K D2              ", k_ring2<4, 4, 6, 16, 2, 0, false>, 512, 0},
-      {"ring2 4c+4l 6x16K D2 nt           ", k_ring2<4, 4, 6, 16, 2, 0, true>, 512, 0},
       {"ring2 4c+2l 6x16K D2              ", k_ring2<4, 2, 6, 16, 2, 0, false>, 384, 0},
-      {"ring2 4c+1l 6x16K D2              ", k_ring2<4, 1, 6, 16, 2, 0, false>, 320, 0},
       {"ring2 4c+4l 8x16K D3              ", k_ring2<4, 4, 8, 16, 3, 0, false>, 512, 0},
-      {"ring2 4c+4l 5x16K D1              ", k_ring2<4, 4, 5, 16, 1, 0, false>, 512, 0},
       {"ring2 4c+4l 4x32K D1              ", k_ring2<4, 4, 4, 32, 1, 0, false>, 512, 0},
       {"ring2 8c+4l 6x16K D2              ", k_ring2<8, 4, 6, 16, 2, 0, false>, 768, 0},
+      {"ring2 4c+4l 8x16K D5              ", k_ring2<4, 4, 8, 16, 5, 0, false>, 512, 0},
+      {"ring2 4c+4l 9x16K D6              ", k_ring2<4, 4, 9, 16, 6, 0, false>, 512, 0},
+      {"ring2 8c+4l 9x16K D6              ", k_ring2<8, 4, 9, 16, 6, 0, false>, 768, 0},
       {"ring2 4c+4l fill-only 6x16K D2    ", k_ring2<4, 4, 6, 16, 2, 1, false>, 512, 1},
+      {"ring2 4c+4l fill-only 8x16K D5    ", k_ring2<4, 4, 8, 16, 5, 1, false>, 512, 1},
+      {"ring2 4c+4l fill-only 9x16K D6    ", k_ring2<4, 4, 9, 16, 6, 1, false>, 512, 1},
       {"ring2 4c consume-only 6x16K       ", k_ring2<4, 4, 6, 16, 2, 2, false>, 512, 2},
       {"ring2 8c consume-only 6x16K       ", k_ring2<8, 4, 6, 16, 2, 2, false>, 768, 2},
   };
   printf("CUs %d; per CU %.2f MB streamed (96 x 32 KB slots); MFMA floor at 4 waves = 96 x 64 x 16 cycles\n",
          ncu, 3.0 * NCHUNK * SLOT / 1048576.0);
+  // (the buffer ADD_TID form, DM 2, is not run: round 6 tested it once — MISMATCH, then the
+  // context was lost — profiles/r06_ring_probe.log)
   for (int rep = 0; rep < (pmc ? 1 : 2); ++rep)
     for (const Var& v : vars) {
       auto launch = [&]() { v.f<<<ncu, v.threads>>>(W, sink, d); };
