@@ -148,3 +148,15 @@ def test_int4_model_matches_oracle(torch, state_dict, golden_model):
     ys = greedy_decode(m4, golden_model["src"], golden_model["src_mask"], 24, 0)
     np.testing.assert_array_equal(ys, o4.greedy_decode(golden_model["src"],
                                                        golden_model["src_mask"], 24))
+
+
+@pytest.mark.parametrize("B,S,max_len", [(3, 13, 23), (2, 9, 18), (5, 31, 37)])
+def test_greedy_ragged_groups_matches_oracle(torch, gpu_model, oracle_model, B, S, max_len):
+    """Source lengths and max_len that are not multiples of 4: the decode's value caches
+    are kept in 4-key groups (k_dec_attn, k_vgroup4; padded last group), so the self cache's
+    last group is partial every step and the cross values' last group is zero-padded."""
+    from qtx.decode import greedy_decode
+    rng = np.random.default_rng(B * 100 + S)
+    src, m = make_batch(rng, B, S)
+    ys = greedy_decode(gpu_model, src, m, max_len, 0)
+    np.testing.assert_array_equal(ys, oracle_model.greedy_decode(src, m, max_len))
