@@ -716,10 +716,15 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
     const int r = min(16 * i + rsub, nrows - 1);
     const long off = (kvb + r) * 512 + h * 64 + 16 * ch;
     const long voff = ((vgb + min(4 * i + vg, glast)) * 512 + h * 64 + vd) * 4;
+#ifdef QTX_KV_DEFAULT_POLICY   // experiment (variant builds): default cache policy on the K/V rows
+    kr[i] = *reinterpret_cast<const uint4*>(a.kc + off);
+    vr[i] = *reinterpret_cast<const uint4*>(a.vc + voff);
+#else
     // non-temporal: each K/V row is read once per step by one wave, so it should not push
     // the weights (re-read every step) out of the XCD's L2 (B = 256: 36.2 -> 35.1 ms)
     kr[i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(a.kc + off)));
     vr[i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(a.vc + voff)));
+#endif
   }
   const int j0 = min(lane, nrows - 1), j1 = min(lane + 64, nrows - 1);
   float sk0 = a.skc[kvb + j0], sk1 = a.skc[kvb + j1];

@@ -9,6 +9,7 @@ O=$GRAFT_REPO_ROOT/gpurun_out/$T
 mkdir -p $O
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
+python -c "import sys; sys.path.insert(0, 'tools'); from prof_summary import sources_sha16; print(sources_sha16())" > $O/sources_sha16.txt
 timeout -k 10 900 python -u -m pytest ${@:-tests} -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?
 tail -3 $O/pytest.log

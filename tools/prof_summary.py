@@ -50,7 +50,11 @@ def main(d):
     rows.sort(key=lambda r: -r["total_ns"])
     tot = sum(r["total_ns"] for r in rows)
     print(f"source: `{os.path.relpath(src)}`  total kernel time {tot / 1e3:.1f} us\n")
-    print(f"kernel_sources_sha16: {sources_sha16()}\n")
+    # the digest of the sources the profiled library was built from: recorded on the GPU box
+    # by tools/gpu_round.sh (<tag>/sources_sha16.txt), else of the sources here
+    rec = os.path.join(os.path.dirname(os.path.abspath(d)), "sources_sha16.txt")
+    sha = open(rec).read().strip() if os.path.exists(rec) else sources_sha16()
+    print(f"kernel_sources_sha16: {sha}\n")
     print("| kernel | calls | total us | avg us | min us | max us | % |")
     print("|---|---:|---:|---:|---:|---:|---:|")
     for r in rows:
