@@ -1,4 +1,5 @@
-"""In-graph cost of each decode-step kernel: N back-to-back launches of one kernel captured
+"""In-graph cost of each decode-step kernel (the product step's amodes since round 6:
+O / Oc and FFN2 quantize their fp32 input from its own rows, A_F32R): N back-to-back launches of one kernel captured
 in a hipGraph (torch.cuda.graph) and replayed — us per launch, to compare with the
 dependent-kernel floor of tools/chain_probe.hip (same stream: every launch waits for the
 previous one, as in the decode step)."""
@@ -84,13 +85,13 @@ cases = {
     "self-attn (k_dec_attn, 41 keys)": lambda st, l: _lib.call(
         "qtx_decode_attention", 1, P(y), 1536, P(KVL[l][0]), P(KVL[l][1]), P(skc), P(svc), 72, P(step), 0, Z, B,
         P(ctx), P(pma), st),
-    "O+res    (A_F32Q, K=512)": skinny(2, ctx, 512, pma, 8, W[(512, 512)], 512, 512, 2, res),
+    "O+res    (A_F32R, K=512)": skinny(3, ctx, 512, None, 0, W[(512, 512)], 512, 512, 2, res),
     "LN+Qc    (A_LN, N=512)": skinny(1, x, 512, None, 0, W[(512, 512)], 512, 512, 0),
     "cross-attn (72 keys)": lambda st, l: _lib.call(
         "qtx_decode_attention", 0, P(y), 512, P(KVL[l][0]), P(KVL[l][1]), P(skc), P(svc), 72, Z, 72, P(mask), B,
         P(ctx), P(pma), st),
-    "LN+FFN1  (A_LN, N=2048, relu+rowmax)": skinny(1, x, 512, None, 0, W[(2048, 512)], 2048, 512, 5, None, pm_out),
-    "FFN2+res (A_F32Q, K=2048)": skinny(2, h, 2048, pmf, 128, W[(512, 2048)], 512, 2048, 2, res),
+    "LN+FFN1  (A_LN, N=2048, relu)": skinny(1, x, 512, None, 0, W[(2048, 512)], 2048, 512, 1),
+    "FFN2+res (A_F32R, K=2048)": skinny(3, h, 2048, None, 0, W[(512, 2048)], 512, 2048, 2, res),
 }
 tot = 0.0
 for name, fn in cases.items():
@@ -102,9 +103,9 @@ print(f"B={B} one decoder layer (8 launches, attention counted as listed): {tot 
 
 # the 8 kernels of a decoder layer in the decode step's order, back to back (different code
 # and data every launch, as in the real step) vs the sum of their single-kernel chains
-order = ["LN+QKV   (A_LN, N=1536)", "self-attn (k_dec_attn, 41 keys)", "O+res    (A_F32Q, K=512)",
-         "LN+Qc    (A_LN, N=512)", "cross-attn (72 keys)", "O+res    (A_F32Q, K=512)",
-         "LN+FFN1  (A_LN, N=2048, relu+rowmax)", "FFN2+res (A_F32Q, K=2048)"]
+order = ["LN+QKV   (A_LN, N=1536)", "self-attn (k_dec_attn, 41 keys)", "O+res    (A_F32R, K=512)",
+         "LN+Qc    (A_LN, N=512)", "cross-attn (72 keys)", "O+res    (A_F32R, K=512)",
+         "LN+FFN1  (A_LN, N=2048, relu)", "FFN2+res (A_F32R, K=2048)"]
 fns = [cases[k] for k in order]
 
 
