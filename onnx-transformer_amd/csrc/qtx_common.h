@@ -305,6 +305,24 @@ __device__ __forceinline__ uint32_t pack4_biased(float t0, float t1, float t2, f
   const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(t3), __float_as_uint(t2), 0x0c0c0400u);
   return __builtin_amdgcn_perm(p23, p01, 0x05040100u);
 }
+// min(max(rint(q), 0), 255) of four quotients packed as bytes: v_cvt_pk_u8_f32 rounds to
+// nearest even, clamps to [0, 255] and maps NaN to 0 (probed against rintf + clamp on halves,
+// near-halves, signed zeros, +-inf and NaN: tools/probe_cvt_pk_u8.hip).  For a quantized ReLU
+// output (codes in [0, 127]) this is the ReLU, the rint and the packing in one op per value:
+// rint(max(y, 0) / s) == max(rint(y / s), 0) for s > 0.
+__device__ __forceinline__ uint32_t pack4_relu_u8(float q0, float q1, float q2, float q3) {
+  uint32_t d = __builtin_amdgcn_cvt_pk_u8_f32(q0, 0u, 0u);
+  d = __builtin_amdgcn_cvt_pk_u8_f32(q1, 1u, d);
+  d = __builtin_amdgcn_cvt_pk_u8_f32(q2, 2u, d);
+  return __builtin_amdgcn_cvt_pk_u8_f32(q3, 3u, d);
+}
+// the codes of four quotients y / s: rint and two's-complement bytes, or, for a ReLU output
+// (RELU), pack4_relu_u8
+template <bool RELU>
+__device__ __forceinline__ uint32_t pack4_codes(float q0, float q1, float q2, float q3) {
+  if constexpr (RELU) return pack4_relu_u8(q0, q1, q2, q3);
+  else return pack4_biased(rint_biased(q0), rint_biased(q1), rint_biased(q2), rint_biased(q3));
+}
 
 // rint(x / s) with the correctly rounded quotient, computed as x * (1/s) except within
 // 2^-13 of a rounding tie, where the true division is taken.  Exact: |x/s| <= ~127, so

@@ -672,9 +672,9 @@ __global__ __launch_bounds__(512) void k_gemm_row(RowGemmArgs g) {
             const int e = ep + h;
             float qv[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) qv[j] = rint_biased(quot(yv(i, j, e), sc[i][e], inv[i][e]));
-            pk[h] = make_uint2(pack4_biased(qv[0], qv[1], qv[2], qv[3]),
-                               pack4_biased(qv[4], qv[5], qv[6], qv[7]));
+            for (int j = 0; j < 8; ++j) qv[j] = quot(yv(i, j, e), sc[i][e], inv[i][e]);
+            pk[h] = make_uint2(pack4_codes<EPI == RE_RELU_QUANT_PMAX>(qv[0], qv[1], qv[2], qv[3]),
+                               pack4_codes<EPI == RE_RELU_QUANT_PMAX>(qv[4], qv[5], qv[6], qv[7]));
           }
           const uint32_t r0 = swap1(odd ? pk[0].x : pk[1].x);
           const uint32_t r1 = swap1(odd ? pk[0].y : pk[1].y);

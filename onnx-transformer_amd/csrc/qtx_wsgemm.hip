@@ -340,10 +340,9 @@ __global__ __launch_bounds__(512) void k_gemm_ws(RowGemmArgs g) {
             uint32_t d[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-              d[j] = pack4_biased(rint_biased(quot(y[i][4 * j], sc[i], inv[i])),
-                                  rint_biased(quot(y[i][4 * j + 1], sc[i], inv[i])),
-                                  rint_biased(quot(y[i][4 * j + 2], sc[i], inv[i])),
-                                  rint_biased(quot(y[i][4 * j + 3], sc[i], inv[i])));
+              d[j] = pack4_codes<EPI == RE_RELU_QUANT_PMAX>(
+                  quot(y[i][4 * j], sc[i], inv[i]), quot(y[i][4 * j + 1], sc[i], inv[i]),
+                  quot(y[i][4 * j + 2], sc[i], inv[i]), quot(y[i][4 * j + 3], sc[i], inv[i]));
             const long row = m0 + 16 * i + f;
             const long off = EPI == RE_QUANT ? row * g.ldo8 + cs : kp_off(row, c0, g.ldo8);
             __builtin_amdgcn_raw_buffer_store_b128(v4u{d[0], d[1], d[2], d[3]}, orsrc, (int)off, 0, 0);
@@ -538,10 +537,9 @@ __global__ __launch_bounds__(512) void k_gemm_wsp(RowGemmArgs g) {
         uint32_t d[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          d[j] = pack4_biased(rint_biased(div_cr(y[i][4 * j] * k2, b, yi)),
-                              rint_biased(div_cr(y[i][4 * j + 1] * k2, b, yi)),
-                              rint_biased(div_cr(y[i][4 * j + 2] * k2, b, yi)),
-                              rint_biased(div_cr(y[i][4 * j + 3] * k2, b, yi)));
+          d[j] = pack4_codes<EPI == RE_RELU_QUANT_PMAX>(
+              div_cr(y[i][4 * j] * k2, b, yi), div_cr(y[i][4 * j + 1] * k2, b, yi),
+              div_cr(y[i][4 * j + 2] * k2, b, yi), div_cr(y[i][4 * j + 3] * k2, b, yi));
         const long row = m0 + 16 * i + f;
         const long off = EPI == RE_QUANT ? row * g.ldo8 + cs : kp_off(row, c0, g.ldo8);
         __builtin_amdgcn_raw_buffer_store_b128(v4u{d[0], d[1], d[2], d[3]}, orsrc, (int)off, 0, 0);
@@ -1033,7 +1031,8 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
 #pragma unroll
     for (int d2 = 0; d2 < 3; ++d2) __builtin_amdgcn_raw_buffer_store_b32(0u, nul, 0, 0, 0);
   };
-  // Y: y of block k (ReLU) from acc and the wave's partial row maxima -> red[k & 1]
+  // Y: y of block k (before the ReLU) from acc and the wave's partial ReLU'd row maxima
+  // -> red[k & 1]
   auto form_y = [&](v4i (&acc)[2][4], float (&y)[2][16], int k) {
     float sr[2];
 #pragma unroll
@@ -1048,7 +1047,9 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          y[i][4 * j + e] = fmaxf(((float)acc[i][j][e] * sr[i]) * swj[e] + bj[e], 0.0f);
+          // pre-ReLU y: the maximum from 0 is the ReLU'd row maximum, and the codes take the
+          // ReLU in their conversion (pack4_relu_u8)
+          y[i][4 * j + e] = ((float)acc[i][j][e] * sr[i]) * swj[e] + bj[e];
           am[i] = fmaxf(am[i], y[i][4 * j + e]);
         }
     }
@@ -1125,10 +1126,8 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
       uint32_t d[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        d[j] = pack4_biased(rint_biased(div_cr(y[i][4 * j], bq[i], iq[i])),
-                            rint_biased(div_cr(y[i][4 * j + 1], bq[i], iq[i])),
-                            rint_biased(div_cr(y[i][4 * j + 2], bq[i], iq[i])),
-                            rint_biased(div_cr(y[i][4 * j + 3], bq[i], iq[i])));
+        d[j] = pack4_relu_u8(div_cr(y[i][4 * j], bq[i], iq[i]), div_cr(y[i][4 * j + 1], bq[i], iq[i]),
+                             div_cr(y[i][4 * j + 2], bq[i], iq[i]), div_cr(y[i][4 * j + 3], bq[i], iq[i]));
       store_row(k, i, d);
     }
   };
@@ -1162,10 +1161,10 @@ __global__ __launch_bounds__(512) void k_gemm_wsy(RowGemmArgs g) {
             float yv = y[ii][4 * jj + e];
             if (s == 0) mfma_pin<true>(acc[i][j], b[j], a[i], hist[LAG - 1], yv);
             else mfma_pin<false>(acc[i][j], b[j], a[i], hist[LAG - 1], yv);
-            tq[e] = rint_biased(div_cr(yv, bq[ii], iq[ii]));
+            tq[e] = div_cr(yv, bq[ii], iq[ii]);
             hist[2] = hist[1]; hist[1] = hist[0]; hist[0] = tq[e];
             if (e == 3) {
-              d[jj] = pack4_biased(tq[0], tq[1], tq[2], tq[3]);
+              d[jj] = pack4_relu_u8(tq[0], tq[1], tq[2], tq[3]);
               if (jj == 3) store_row(kq, ii, d);
             }
           }
