@@ -428,21 +428,27 @@ def test_linear_rows_ws_qkv_scales(torch, M):
         np.testing.assert_array_equal(os_[t].cpu().numpy(), s)
 
 
-@pytest.mark.parametrize("M", [300, 7, 20011, 4096, 64, 32768])
-def test_linear_rows_ws_ffn1_onepass_scales(torch, M):
+@pytest.mark.parametrize("M,neg", [(300, False), (7, False), (20011, False), (4096, False), (64, False),
+                                   (32768, False), (300, True), (4096, True)])
+def test_linear_rows_ws_ffn1_onepass_scales(torch, M, neg):
     """FFN1 in one pass (kp = 3: ReLU + per-token quantization over all 2048 columns, the
     4 column slices' row maxima exchanged inside the launch) on k_gemm_wsy (quantization
     between the MFMAs), with row scales from 1e-35 to 1e25; bit-exact, and the exchange
-    never timed out (status word 0).  (kp = 4 / 5, the 32x32x32-MFMA variants: diagnostic
-    build, tests/diag_variants.py.)"""
+    never timed out (status word 0).  neg: a negative bias and every third row of x zero, so
+    those rows are all below zero before the ReLU (row maximum 0, scale 1e-5 / 127, and
+    pre-ReLU quotients down to -1e10 that the code conversion must clamp to 0).  (kp = 4 / 5,
+    the 32x32x32-MFMA variants: diagnostic build, tests/diag_variants.py.)"""
     kp = 3
     from qtx._lib import lib
     wsy = 1
-    rng = np.random.default_rng(M + 31 * wsy)
+    rng = np.random.default_rng(M + 31 * wsy + 7 * neg)
     qx, sx = O.quant_rows(rng.standard_normal((M, 512)).astype(f32))
     sx = (sx * np.float32(10.0) ** rng.integers(-33, 26, M)).astype(f32)
     qw, sw = O.quant_weight((rng.standard_normal((2048, 512)) * 0.05).astype(f32), 8)
     b = (rng.standard_normal(2048) * 1e-3).astype(f32)
+    if neg:
+        b = (-np.abs(b) * 1e3 - 1e-3).astype(f32)
+        qx[::3] = 0
     wk = torch.empty((2048, 512), dtype=torch.int8, device="cuda")
     assert lib().qtx_pack_w_ws(P(dev(torch, qw)), 2048, 512, P(wk), S0) == 0
     h8 = torch.zeros((M + (M & 1), 2048), dtype=torch.int8, device="cuda")
@@ -454,6 +460,8 @@ def test_linear_rows_ws_ffn1_onepass_scales(torch, M):
                ldo8=2048, os=sh)
     h = O.linear_epilogue(O.int_gemm(qx, qw), sx, sw, b, relu=True)
     qh, s = O.quant_rows(h)
+    if neg:
+        assert (s[::3] == np.float32(1e-5) / np.float32(127)).all() and not qh[::3].any()
     np.testing.assert_array_equal(_from_kp(h8.cpu().numpy(), M), qh)
     np.testing.assert_array_equal(sh.cpu().numpy(), s)
     status = gx.view(torch.int32)[2 * (4 * 32 * nb) + 1].item()
