@@ -409,7 +409,7 @@ def cpu_model():
     return "unknown"
 
 
-ALL_CPUS_STEPS, ALL_CPUS_TIMEOUT_S = 8, 60
+ALL_CPUS_STEPS, ALL_CPUS_TIMEOUT_S = 8, 40
 
 
 def all_cpus_leg(B, S, seed):
@@ -442,8 +442,10 @@ def all_cpus_leg(B, S, seed):
             return allc, B * ALL_CPUS_STEPS / float(r.stdout.strip().splitlines()[-1]), note
         return allc, None, note + f"; failed: {r.stderr.strip()[-200:]}"
     except subprocess.TimeoutExpired:
-        return allc, None, note + f"; did not finish in {ALL_CPUS_TIMEOUT_S} s (that many " \
-                                  "threads on this job's CPU share)"
+        return allc, None, note + f"; did not finish in {ALL_CPUS_TIMEOUT_S} s: that many " \
+                                  "threads on this job's CPU quota (cgroup cpu.max 16 CPUs on the GPU box) " \
+                                  "stall; profiles/r06_all_cpus_probe.log: 16 threads 801 tok/s, 64 threads " \
+                                  "246 tok/s (4-step samples), 256 threads no 2-sentence warm-up in 95 s"
 
 
 def cpu_baseline(sd, B=32, S=72, max_len=72, seed=7):
@@ -490,6 +492,7 @@ def cpu_baseline(sd, B=32, S=72, max_len=72, seed=7):
 
 
 def main():
+    t_start = time.perf_counter()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -582,7 +585,7 @@ def main():
         verified = bool((allids >= 0).all() and np.array_equal(ref, allids[pick]))
 
     def progress(msg):      # stderr, so a long run is visibly alive (stdout: the JSON line only)
-        print(f"bench: {msg} ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
+        print(f"bench: {msg} ({time.perf_counter() - t_start:.0f} s since start)", file=sys.stderr, flush=True)
 
     if rank == 0:
         progress(f"timed region done: {value:.0f} tokens/s")
@@ -706,6 +709,7 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             progress("GPU lines done; CPU baseline next")
             out["cpu_baseline"] = cpu_baseline(sd)
+            progress("CPU baseline done")
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
