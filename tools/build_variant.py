@@ -15,7 +15,7 @@ from qtx import _build  # noqa: E402
 
 def main():
     out, extra = os.path.abspath(sys.argv[1]), sys.argv[2:]
-    objdir = os.path.join(REPO, "onnx-transformer_amd", "qtx", "build_obj_variant")
+    objdir = os.path.join(REPO, "onnx-transformer_amd", "qtx", "build_obj_variant" + os.environ.get("QTX_VARIANT_TAG", ""))
     os.makedirs(objdir, exist_ok=True)
     cflags = [f for f in _build.FLAGS if f != "-shared"] + extra
 
