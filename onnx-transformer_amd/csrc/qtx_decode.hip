@@ -854,28 +854,41 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   // ds_read_b32 per chain step of 4 keys, each byte converted by one SDWA v_cvt_f32_i32.
   float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
   const uint32_t* vl = reinterpret_cast<const uint32_t*>(Vs) + lane;
-#pragma unroll 2
-  for (int g = 0; g < nk16; g += 16) {
-    const float4 p0 = *reinterpret_cast<const float4*>(PS + g);
-    const float4 p1 = *reinterpret_cast<const float4*>(PS + g + 4);
-    const float4 p2 = *reinterpret_cast<const float4*>(PS + g + 8);
-    const float4 p3 = *reinterpret_cast<const float4*>(PS + g + 12);
-    float v[16];
+  // every 16-key group's operands are read first (the NIT groups that cover the staged rows;
+  // those at or past nk16 are read and not used), so the chains pay the LDS latency once
+  // instead of once per group (a rolled loop waited on its reads every 16 keys)
+  float4 pg[NIT][4];
+  uint32_t vg4[NIT][4];
+#pragma unroll
+  for (int g = 0; g < NIT; ++g) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint32_t d = vl[(g / 4 + q) * 64];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[4 * q + e] = (float)(int8_t)(d >> (8 * e));
+      pg[g][q] = *reinterpret_cast<const float4*>(PS + 16 * g + 4 * q);
+      vg4[g][q] = vl[(4 * g + q) * 64];
     }
-    // each fma an asm v_fmac_f32 (the IEEE fused multiply-add, as fmaf): left to itself the
-    // compiler SLP-packs the four chains into v_pk_fma_f32 pairs — no faster on gfx950 (a
-    // packed fp32 op issues at half rate) — and assembles their operand pairs with ~1 v_mov
-    // per fma
-    auto fmac = [](float& c, float p, float x) { asm("v_fmac_f32 %0, %1, %2" : "+v"(c) : "v"(p), "v"(x)); };
-    fmac(c0, p0.x, v[0]);  fmac(c1, p1.x, v[4]);  fmac(c2, p2.x, v[8]);  fmac(c3, p3.x, v[12]);
-    fmac(c0, p0.y, v[1]);  fmac(c1, p1.y, v[5]);  fmac(c2, p2.y, v[9]);  fmac(c3, p3.y, v[13]);
-    fmac(c0, p0.z, v[2]);  fmac(c1, p1.z, v[6]);  fmac(c2, p2.z, v[10]); fmac(c3, p3.z, v[14]);
-    fmac(c0, p0.w, v[3]);  fmac(c1, p1.w, v[7]);  fmac(c2, p2.w, v[11]); fmac(c3, p3.w, v[15]);
+    // in group order (LDS returns in issue order: the first chains then wait for group 0
+    // alone, which the scheduler would otherwise issue last)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // each fma an asm v_fmac_f32 (the IEEE fused multiply-add, as fmaf): left to itself the
+  // compiler SLP-packs the four chains into v_pk_fma_f32 pairs — no faster on gfx950 (a
+  // packed fp32 op issues at half rate) — and assembles their operand pairs with ~1 v_mov
+  // per fma
+  auto fmac = [](float& c, float p, float x) { asm("v_fmac_f32 %0, %1, %2" : "+v"(c) : "v"(p), "v"(x)); };
+#pragma unroll
+  for (int g = 0; g < NIT; ++g) {
+    if (g == 0 || 16 * g < nk16) {       // (Sk >= 1: group 0 always)
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = (float)(int8_t)(vg4[g][q] >> (8 * e));
+      const float4 p0 = pg[g][0], p1 = pg[g][1], p2 = pg[g][2], p3 = pg[g][3];
+      fmac(c0, p0.x, v[0]);  fmac(c1, p1.x, v[4]);  fmac(c2, p2.x, v[8]);  fmac(c3, p3.x, v[12]);
+      fmac(c0, p0.y, v[1]);  fmac(c1, p1.y, v[5]);  fmac(c2, p2.y, v[9]);  fmac(c3, p3.y, v[13]);
+      fmac(c0, p0.z, v[2]);  fmac(c1, p1.z, v[6]);  fmac(c2, p2.z, v[10]); fmac(c3, p3.z, v[14]);
+      fmac(c0, p0.w, v[3]);  fmac(c1, p1.w, v[7]);  fmac(c2, p2.w, v[11]); fmac(c3, p3.w, v[15]);
+    }
   }
   const float acc = (c0 + c1) + (c2 + c3);
   QTX_STAMP(3);
