@@ -201,12 +201,13 @@ def test_embed(torch, gpu_model, golden_ops, oracle_model):
                                   oracle_model.embed(ids[:, :5] % 4444, oracle_model.tgt_lut, pos0=9))
 
 
-@pytest.mark.parametrize("M", [37, 32, 5])
+@pytest.mark.parametrize("M", [37, 32, 5, 100, 256])
 def test_generator(torch, gpu_model, golden_ops, oracle_model, M):
     """Logits bit-exact (fp32-MFMA chain == the oracle's sequential fma chain), argmax
-    exact, log-probs within the platform log's ulp; M <= 32 takes the decode's small-batch
-    workgroup shape (fewer strips per workgroup)."""
-    x = (np.concatenate([golden_ops["gen_x"]] * 10)[:M]
+    exact, log-probs within the platform log's ulp; M > 32 runs several 16-row blocks per
+    workgroup under one load of the weight strips (ragged last group at M = 37 and 100)."""
+    gx = golden_ops["gen_x"]
+    x = (np.concatenate([gx] * (M // len(gx) + 1))[:M]
          * np.linspace(0.1, 3, M, dtype=f32)[:, None]).astype(f32)
     logp, ids, logits = gpu_model.generator(dev(torch, x), return_logits=True)
     np.testing.assert_array_equal(logits.cpu().numpy(), oracle_model.logits(x))
