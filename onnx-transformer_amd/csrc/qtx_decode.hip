@@ -710,29 +710,31 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   // values: per 16 keys, 4 groups x this head's 64 dims x 4 B = 1 KB, lane = group
   // 4 i + lane / 16, dims 4 (lane % 16) .. + 3
   const int vg = lane >> 4, vd = 4 * (lane & 15), glast = (nrows - 1) >> 2;
+  // wave-uniform bases of this head's rows and 32-bit lane offsets: the loads take the
+  // scalar-base + vector-offset form instead of 64-bit address arithmetic per load
+  const int8_t* const kbase = a.kc + kvb * 512 + h * 64;
+  const int8_t* const vbase = a.vc + vgb * 2048 + h * 256;
   uint4 kr[NIT], vr[NIT];
 #pragma unroll
   for (int i = 0; i < NIT; ++i) {
-    const int r = min(16 * i + rsub, nrows - 1);
-    const long off = (kvb + r) * 512 + h * 64 + 16 * ch;
-    const long voff = ((vgb + min(4 * i + vg, glast)) * 512 + h * 64 + vd) * 4;
-#ifdef QTX_KV_DEFAULT_POLICY   // experiment (variant builds): default cache policy on the K/V rows
-    kr[i] = *reinterpret_cast<const uint4*>(a.kc + off);
-    vr[i] = *reinterpret_cast<const uint4*>(a.vc + voff);
-#else
+    const unsigned koff = (unsigned)(min(16 * i + rsub, nrows - 1) * 512 + 16 * ch);
+    const unsigned voff = (unsigned)(min(4 * i + vg, glast) * 2048 + 4 * vd);
     // non-temporal: each K/V row is read once per step by one wave, so it should not push
-    // the weights (re-read every step) out of the XCD's L2 (B = 256: 36.2 -> 35.1 ms)
-    kr[i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(a.kc + off)));
-    vr[i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(a.vc + voff)));
-#endif
+    // the weights (re-read every step) out of the XCD's L2 (B = 256: 36.2 -> 35.1 ms; the
+    // default policy re-measured in round 6: B = 32 12.87 vs 12.84, B = 256 26.25 vs 25.58 ms)
+    kr[i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(kbase + koff)));
+    vr[i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(vbase + voff)));
   }
   const int j0 = min(lane, nrows - 1), j1 = min(lane + 64, nrows - 1);
-  float sk0 = a.skc[kvb + j0], sk1 = a.skc[kvb + j1];
-  const float sv0 = a.svc[kvb + j0], sv1 = a.svc[kvb + j1];
+  const float* const skb = a.skc + kvb;
+  const float* const svb = a.svc + kvb;
+  float sk0 = skb[(unsigned)j0], sk1 = skb[(unsigned)j1];
+  const float sv0 = svb[(unsigned)j0], sv1 = svb[(unsigned)j1];
   bool keep0 = true, keep1 = true;
   if constexpr (!KV_NEW) {
-    keep0 = a.mask[(long)b * a.S + j0] != 0;
-    keep1 = a.mask[(long)b * a.S + j1] != 0;
+    const uint8_t* const mb = a.mask + (long)b * a.S;
+    keep0 = mb[(unsigned)j0] != 0;
+    keep1 = mb[(unsigned)j1] != 0;
   }
   // cross: keys past the sentence's last unmasked one contribute exactly nothing (score
   // -1e9 -> qexp 0 -> P 0, and fma(0, v, acc) == acc), so the key loops stop there; a
