@@ -295,6 +295,15 @@ __host__ __device__ __forceinline__ long kp_off(long r, long k, long K) {
   return (((r >> 1) * (K >> 6) + (k >> 6)) << 7) + ((r & 1) << 6) + (k & 63);
 }
 
+// *(T*)((char*)base + byte_off) with a 32-bit unsigned byte offset: for a wave-uniform base
+// (a kernel argument) the compiler emits the scalar-base + vector-offset global load instead
+// of 64-bit address arithmetic per load (in the latency-bound decode kernels the
+// instructions before a kernel's loads are on its critical path)
+template <class T>
+__device__ __forceinline__ const T& ld_at(const T* base, unsigned byte_off) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
 // rint(q) packed as int8 for |q| <= 2^22: RN(q + 1.5 * 2^23) is 1.5 * 2^23 + rint(q)
 // (the add rounds to an integer, ties to even, exactly as rintf: 1.5 * 2^23 is even), so
 // the low byte of its bit pattern is rint(q) in two's complement.  One add per value plus

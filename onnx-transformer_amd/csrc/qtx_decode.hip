@@ -62,7 +62,7 @@ __device__ __forceinline__ void skinny_prologue(const SkinnyArgs& g, uint8_t* As
 #pragma unroll
     for (int j = 0; j < NLD; ++j) {
       const int idx = min(tid + 256 * j, TOT - 1), m = min(m0 + idx / CPR, g.M - 1);
-      v[j] = *reinterpret_cast<const uint4*>(g.A + (long)m * K + 16 * (idx % CPR));
+      v[j] = ld_at(reinterpret_cast<const uint4*>(g.A), (unsigned)(m * K + 16 * (idx % CPR)));
     }
     issue_rest();
     if (tid < BM) sas[tid] = (tid < RB && m0 + tid < g.M) ? g.sa[m0 + tid] : 0.0f;
@@ -80,7 +80,7 @@ __device__ __forceinline__ void skinny_prologue(const SkinnyArgs& g, uint8_t* As
       const int m = min(m0 + wave + 4 * j, g.M - 1);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const float4 t = *reinterpret_cast<const float4*>(g.X + (long)m * g.ldx + 4 * (lane + 64 * c));
+        const float4 t = ld_at(reinterpret_cast<const float4*>(g.X), 4u * (unsigned)(m * (int)g.ldx + 4 * (lane + 64 * c)));
         v[j][c][0] = t.x; v[j][c][1] = t.y; v[j][c][2] = t.z; v[j][c][3] = t.w;
       }
     }
@@ -120,11 +120,11 @@ __device__ __forceinline__ void skinny_prologue(const SkinnyArgs& g, uint8_t* As
         const int m = min(m0 + wave + 4 * (j0 + jb), g.M - 1);
 #pragma unroll
         for (int c = 0; c < NC; ++c)
-          t[jb][c] = *reinterpret_cast<const float4*>(g.X + (long)m * g.ldx + 4 * (lane + 64 * c));
+          t[jb][c] = ld_at(reinterpret_cast<const float4*>(g.X), 4u * (unsigned)(m * (int)g.ldx + 4 * (lane + 64 * c)));
         if constexpr (!OWN)
 #pragma unroll
           for (int u = 0; u < 2; ++u)   // lane takes partials lane, lane+64 (clamped: max-safe)
-            pm[jb][u] = g.pmax_in[(long)min(lane + 64 * u, g.pmax_n - 1) * g.M + m];
+            pm[jb][u] = ld_at(g.pmax_in, 4u * (unsigned)(min(lane + 64 * u, g.pmax_n - 1) * g.M + m));
       }
       if (j0 == 0) issue_rest();
 #pragma unroll
@@ -199,22 +199,22 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
       wf[s] = make_uint4(n + k, k, n, 1); wp[s] = make_uint2(n, k);
 #else
       if constexpr (WBITS == 8)
-        wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + k);
+        wf[s] = ld_at(reinterpret_cast<const uint4*>(g.W), (unsigned)(n * (int)g.ldw + k));
       else
-        wp[s] = *reinterpret_cast<const uint2*>(g.W + (long)n * g.ldw + (k >> 1));
+        wp[s] = ld_at(reinterpret_cast<const uint2*>(g.W), (unsigned)(n * (int)g.ldw + (k >> 1)));
 #endif
     }
     // every wave, unconditionally, at clamped addresses (values of rows / columns outside
     // the tile are never stored): a load under a branch makes the compiler's vmcnt for the
     // prologue's own loads count the branch-free path, i.e. wait for the weights too
     const int cc = min(col, g.N - 1);
-    swc = g.sw[cc];
-    bc = g.bias[cc];
+    swc = ld_at(g.sw, 4u * cc);
+    bc = ld_at(g.bias, 4u * cc);
     if constexpr (resid) {   // the rows this wave finishes: 4 fg + wave of each tile
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
         const int row = min(m0 + 16 * i + 4 * fg + wave, g.M - 1);
-        rv[i] = g.res[(long)row * g.ldr + cc];
+        rv[i] = ld_at(g.res, 4u * (unsigned)(row * (int)g.ldr + cc));
       }
     }
   };
@@ -308,22 +308,22 @@ __global__ __launch_bounds__(512) void k_skinny8_ffn2(SkinnyArgs g) {
   float4 t[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c)
-    t[c] = *reinterpret_cast<const float4*>(g.X + (long)m * g.ldx + 4 * (lane + 64 * (4 * half + c)));
+    t[c] = ld_at(reinterpret_cast<const float4*>(g.X), 4u * (unsigned)(m * (int)g.ldx + 4 * (lane + 64 * (4 * half + c))));
   float pm[2] = {0.0f, 0.0f};
   if constexpr (!OWN)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) pm[u] = g.pmax_in[(long)min(lane + 64 * u, g.pmax_n - 1) * g.M + m];
+    for (int u = 0; u < 2; ++u) pm[u] = ld_at(g.pmax_in, 4u * (unsigned)(min(lane + 64 * u, g.pmax_n - 1) * g.M + m));
   // 2. then this wave's weight fragments and (wave 0) the epilogue operands
   const int n = min(n0 + fr, g.N - 1);
   uint4 wf[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s)
-    wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + wave * KW + 64 * s + 16 * fg);
+    wf[s] = ld_at(reinterpret_cast<const uint4*>(g.W), (unsigned)(n * (int)g.ldw + wave * KW + 64 * s + 16 * fg));
   const int col = n0 + fr, cc = min(col, g.N - 1);
   const bool cok = col < g.N;
-  const float swc = g.sw[cc], bc = g.bias[cc];
+  const float swc = ld_at(g.sw, 4u * cc), bc = ld_at(g.bias, 4u * cc);
   // the epilogue's output of this lane (wave 0): row m0 + (lane >> 4), column n0 + (lane & 15)
-  const float rv = g.res[(long)min(m0 + fg, g.M - 1) * g.ldr + cc];
+  const float rv = ld_at(g.res, 4u * (unsigned)(min(m0 + fg, g.M - 1) * (int)g.ldr + cc));
   // 3. per-token quantization of the half row into LDS
   {
     const bool ok = m0 + r < g.M;
@@ -418,26 +418,26 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
       wf[s] = make_uint4(n + k, k, n, 1); wp[s] = make_uint2(n, k);
 #else
       if constexpr (WBITS == 8)
-        wf[s] = *reinterpret_cast<const uint4*>(g.W + (long)n * g.ldw + k);
+        wf[s] = ld_at(reinterpret_cast<const uint4*>(g.W), (unsigned)(n * (int)g.ldw + k));
       else
-        wp[s] = *reinterpret_cast<const uint2*>(g.W + (long)n * g.ldw + (k >> 1));
+        wp[s] = ld_at(reinterpret_cast<const uint2*>(g.W), (unsigned)(n * (int)g.ldw + (k >> 1)));
 #endif
     }
-    swc = cok ? g.sw[col] : 0.0f;
-    bc = cok ? g.bias[col] : 0.0f;
+    swc = cok ? ld_at(g.sw, 4u * col) : 0.0f;
+    bc = cok ? ld_at(g.bias, 4u * col) : 0.0f;
     if constexpr (RB == 4) {   // the epilogue's one output per lane: row m0 + fg
-      rv[0] = (resid && cok && m0 + fg < g.M) ? g.res[(long)(m0 + fg) * g.ldr + col] : 0.0f;
+      rv[0] = (resid && cok && m0 + fg < g.M) ? ld_at(g.res, 4u * (unsigned)((m0 + fg) * (int)g.ldr + col)) : 0.0f;
     } else if constexpr (RB == 8) {   // its two: rows m0 + fg, m0 + fg + 4
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int row = m0 + fg + 4 * j;
-        rv[j] = (resid && cok && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
+        rv[j] = (resid && cok && row < g.M) ? ld_at(g.res, 4u * (unsigned)(row * (int)g.ldr + col)) : 0.0f;
       }
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * fg + e, row = m0 + r;
-        rv[e] = (resid && cok && r < RB && row < g.M) ? g.res[(long)row * g.ldr + col] : 0.0f;
+        rv[e] = (resid && cok && r < RB && row < g.M) ? ld_at(g.res, 4u * (unsigned)(row * (int)g.ldr + col)) : 0.0f;
       }
     }
   };
@@ -649,6 +649,11 @@ hipError_t skinny_mode(const SkinnyArgs& g, hipStream_t st) {
 hipError_t launch_skinny(const SkinnyArgs& g, int wbits, hipStream_t st) {
   if (g.M <= 0) return hipSuccess;
   if (g.N % 16) return hipErrorInvalidValue;
+  // the kernels address X / res / A / W with 32-bit byte offsets (ld_at)
+  const long lim = 1L << 30;
+  if ((long)g.M * (g.ldx > g.K ? g.ldx : g.K) >= lim || (long)g.M * g.ldr >= lim ||
+      (long)g.N * g.ldw >= lim || (long)g.M * g.pmax_n >= lim)
+    return hipErrorInvalidValue;
   if (wbits == 8) return skinny_mode<8>(g, st);
   if (wbits == 4) return skinny_mode<4>(g, st);
   return hipErrorInvalidValue;
