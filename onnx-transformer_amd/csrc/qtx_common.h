@@ -303,6 +303,10 @@ template <class T>
 __device__ __forceinline__ const T& ld_at(const T* base, unsigned byte_off) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
 }
+template <class T>
+__device__ __forceinline__ void st_at(T* base, unsigned byte_off, const T& v) {
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off) = v;
+}
 
 // rint(q) packed as int8 for |q| <= 2^22: RN(q + 1.5 * 2^23) is 1.5 * 2^23 + rint(q)
 // (the add rounds to an integer, ties to even, exactly as rintf: 1.5 * 2^23 is even), so

@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void k_skinny(SkinnyArgs g) {
       float y = ((float)sum * sas[r]) * swc + bc;
       if constexpr (relu) y = y > 0.0f ? y : 0.0f;
       if constexpr (resid) y = rv[i] + y;
-      if (ok) g.out[(long)row * g.ldo + col] = y;
+      if (ok) st_at(g.out, 4u * (unsigned)(row * (int)g.ldo + col), y);
       if constexpr (rmax) {
         float am = ok ? fabsf(y) : 0.0f;   // max over the 16 lanes (columns) of this row
         am = fmaxf(am, dpp<0xB1>(am));
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(512) void k_skinny8_ffn2(SkinnyArgs g) {
     for (int w = 0; w < 8; ++w) sum += reinterpret_cast<const int*>(&red[w][src])[e];
     const int row = m0 + e;
     const float y = ((float)sum * sas[e]) * swc + bc;
-    if (cok && row < g.M) g.out[(long)row * g.ldo + col] = rv + y;
+    if (cok && row < g.M) st_at(g.out, 4u * (unsigned)(row * (int)g.ldo + col), rv + y);
   }
 }
 
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
     float y = ((float)v * sas[fg]) * swc + bc;
     if constexpr (relu) y = y > 0.0f ? y : 0.0f;
     if constexpr (resid) y = rv[0] + y;
-    if (ok) g.out[(long)row * g.ldo + col] = y;
+    if (ok) st_at(g.out, 4u * (unsigned)(row * (int)g.ldo + col), y);
     if constexpr (rmax) {
       float am = ok ? fabsf(y) : 0.0f;   // max over the 16 lanes (columns) of this row
       am = fmaxf(am, dpp<0xB1>(am));
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
       float y = ((float)v * sas[r]) * swc + bc;
       if constexpr (relu) y = y > 0.0f ? y : 0.0f;
       if constexpr (resid) y = rv[j] + y;
-      if (ok) g.out[(long)row * g.ldo + col] = y;
+      if (ok) st_at(g.out, 4u * (unsigned)(row * (int)g.ldo + col), y);
       if constexpr (rmax) {
         float am = ok ? fabsf(y) : 0.0f;   // max over the 16 lanes (columns) of this row
         am = fmaxf(am, dpp<0xB1>(am));
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(256) void k_skinny_wide(SkinnyArgs g) {
     float y = ((float)acc[e] * sas[r]) * swc + bc;
     if constexpr (relu) y = y > 0.0f ? y : 0.0f;
     if constexpr (resid) y = rv[e] + y;
-    if (ok) g.out[(long)row * g.ldo + col] = y;
+    if (ok) st_at(g.out, 4u * (unsigned)(row * (int)g.ldo + col), y);
     if constexpr (rmax) {
       float am = ok ? fabsf(y) : 0.0f;   // max over the 16 lanes (columns) of this row
       am = fmaxf(am, dpp<0xB1>(am));
@@ -652,7 +652,7 @@ hipError_t launch_skinny(const SkinnyArgs& g, int wbits, hipStream_t st) {
   // the kernels address X / res / A / W with 32-bit byte offsets (ld_at)
   const long lim = 1L << 30;
   if ((long)g.M * (g.ldx > g.K ? g.ldx : g.K) >= lim || (long)g.M * g.ldr >= lim ||
-      (long)g.N * g.ldw >= lim || (long)g.M * g.pmax_n >= lim)
+      (long)g.M * g.ldo >= lim || (long)g.N * g.ldw >= lim || (long)g.M * g.pmax_n >= lim)
     return hipErrorInvalidValue;
   if (wbits == 8) return skinny_mode<8>(g, st);
   if (wbits == 4) return skinny_mode<4>(g, st);
@@ -903,7 +903,7 @@ __global__ __launch_bounds__(64) void k_dec_attn(DecAttnArgs a) {
   // phase 5: this head's 64 context values (and their absmax when asked for: the consumer
   // GEMM then takes the row maximum over the 8 heads, A_F32Q; the fused decode's consumer
   // forms it from the row itself, A_F32R)
-  a.ctx[(long)b * 512 + h * 64 + lane] = acc;
+  st_at(a.ctx, 4u * (unsigned)(b * 512 + h * 64 + lane), acc);
   if (a.pmax) {
     const float am = wave_max(fabsf(acc));
     if (lane == 0) a.pmax[(long)h * a.B + b] = am;
@@ -1041,8 +1041,8 @@ __global__ __launch_bounds__(1024) void k_generator_mfma(const float* x, long ld
   const int sw = wave & 3, qq = wave >> 2;          // strip within the group, k-quarter
   // blockIdx -> (strip group g, row block rb): hw = 8 (nrb (g / 8) + rb) + g % 8, so the
   // row blocks of group g share hw % 8 (one XCD under round-robin placement)
-  const int nrb = (M + 15) / 16, hw = blockIdx.x;
-  const int rb = (hw >> 3) % nrb, g = ((hw >> 3) / nrb) * 8 + (hw & 7);
+  const unsigned nrb = (unsigned)(M + 15) >> 4, hw = blockIdx.x;   // (unsigned: a shorter division)
+  const int rb = (int)((hw >> 3) % nrb), g = (int)(((hw >> 3) / nrb) * 8 + (hw & 7));
   const int nstrip = (V + 15) / 16, strip = g * 4 + sw;
   if (g * 4 >= nstrip) return;                     // whole block (uniform)
   const int m0 = rb * 16;
@@ -1050,19 +1050,18 @@ __global__ __launch_bounds__(1024) void k_generator_mfma(const float* x, long ld
   QTX_STAMP(0);
   // 1. the quarter strip's B operands, all in flight before anything else
   constexpr int QQ = GEN_Q / 4;
-  const float4* wp = reinterpret_cast<const float4*>(Wm) +
-                     ((long)min(strip, nstrip - 1) * GEN_Q + QQ * qq) * 64 + lane;
+  const unsigned wo = 16u * (unsigned)((min(strip, nstrip - 1) * GEN_Q + QQ * qq) * 64 + lane);
   float4 wq[QQ];
 #pragma unroll
-  for (int q = 0; q < QQ; ++q) wq[q] = wp[q * 64];
-  const float bv = bias[min(vcol, V - 1)];
+  for (int q = 0; q < QQ; ++q) wq[q] = ld_at(reinterpret_cast<const float4*>(Wm), wo + 1024u * q);
+  const float bv = ld_at(bias, 4u * min(vcol, V - 1));
   // 2. row `wave` of the block, LayerNorm in the canonical order, into LDS
   float xv[1][2][4];
   {
     const int m = min(m0 + wave, M - 1);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      const float4 t = *reinterpret_cast<const float4*>(x + (long)m * ldx + 4 * (lane + 64 * c));
+      const float4 t = ld_at(reinterpret_cast<const float4*>(x), 4u * (unsigned)(m * (int)ldx + 4 * (lane + 64 * c)));
       xv[0][c][0] = t.x; xv[0][c][1] = t.y; xv[0][c][2] = t.z; xv[0][c][3] = t.w;
     }
   }
@@ -1095,7 +1094,7 @@ __global__ __launch_bounds__(1024) void k_generator_mfma(const float* x, long ld
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int m = m0 + 4 * fg + e;
-    if (m < M) logits[(long)m * V + vcol] = ((acc[e] + p1[e]) + (p2[e] + p3[e])) + bv;
+    if (m < M) st_at(logits, 4u * (unsigned)(m * V + vcol), ((acc[e] + p1[e]) + (p2[e] + p3[e])) + bv);
   }
   QTX_STAMP(3);
 }
@@ -1104,6 +1103,7 @@ hipError_t launch_generator_mfma(const float* x, long ldx, int M, const float* l
                                  const float* ln_b, const float* Wm, const float* b, int V,
                                  float* logits, hipStream_t st) {
   if (M <= 0) return hipSuccess;
+  if ((long)M * V >= (1L << 30) || (long)M * ldx >= (1L << 30)) return hipErrorInvalidValue;   // 32-bit offsets
   const int ngroup = (V + 63) / 64, nrb = (M + 15) / 16;
   const unsigned grid = 8u * nrb * ((ngroup + 7) / 8);
   k_generator_mfma<<<dim3(grid), dim3(1024), 0, st>>>(x, ldx, M, ln_a, ln_b, Wm, b, V, logits);
@@ -1193,12 +1193,12 @@ __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int 
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   QTX_STAMP(0);
   const int s = host_s1 > 0 ? host_s1 - 1 : *step;
-  const float* x = logits + (long)m * V;
+  const unsigned xo = 4u * (unsigned)(m * V);
   float4 pe_row = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // position s+1 is known up front
-  if (tid < 128) pe_row = *reinterpret_cast<const float4*>(pe + (long)min(s + 1, max_pos - 1) * 512 + 4 * tid);
+  if (tid < 128) pe_row = ld_at(reinterpret_cast<const float4*>(pe), 16u * (unsigned)(min(s + 1, max_pos - 1) * 128 + tid));
   float t[ARG_NV];
 #pragma unroll
-  for (int i = 0; i < ARG_NV; ++i) t[i] = x[min(tid + ARG_T * i, V - 1)];   // clamped
+  for (int i = 0; i < ARG_NV; ++i) t[i] = ld_at(logits, xo + 4u * min(tid + ARG_T * i, V - 1));   // clamped
   QTX_STAMP(1);
   // max: order-free; every wave reduces the 16 wave maxima itself (no second barrier);
   // with it the non-finite test: bit 0 = a NaN or +inf, bit 1 = a value above -inf
@@ -1282,10 +1282,10 @@ __global__ __launch_bounds__(1024) void k_argmax_embed(const float* logits, int 
   // next decoder input: tgt_embed(id) at position s + 1 (embeddings.py:12-13)
   if (tid < 128) {
     const float sc = 0x1.6a09e6p+4f;
-    const float4 e = *reinterpret_cast<const float4*>(lut + (long)id * 512 + 4 * tid);
+    const float4 e = ld_at(reinterpret_cast<const float4*>(lut), 16u * (unsigned)(id * 128 + tid));
     const float4 q = pe_row;
-    *reinterpret_cast<float4*>(xnext + (long)m * 512 + 4 * tid) =
-        make_float4(e.x * sc + q.x, e.y * sc + q.y, e.z * sc + q.z, e.w * sc + q.w);
+    st_at(reinterpret_cast<float4*>(xnext), 16u * (unsigned)(m * 128 + tid),
+          make_float4(e.x * sc + q.x, e.y * sc + q.y, e.z * sc + q.z, e.w * sc + q.w));
   }
   QTX_STAMP(5);
   // every workgroup has read *step above; the last one to arrive advances it
@@ -1302,7 +1302,7 @@ hipError_t launch_argmax_embed(const float* logits, int M, int V, int64_t* ids, 
                                int* step, unsigned* arrive, const float* lut, const float* pe,
                                int max_pos, float* xnext, hipStream_t st, int host_s1) {
   if (M <= 0) return hipSuccess;
-  if (V > ARG_MAXV || host_s1 < 0) return hipErrorInvalidValue;
+  if (V > ARG_MAXV || host_s1 < 0 || (long)M * V >= (1L << 30)) return hipErrorInvalidValue;
   k_argmax_embed<<<dim3(M), dim3(ARG_T), 0, st>>>(logits, V, ids, ids_bs, step, arrive, lut,
                                                   pe, max_pos, xnext, host_s1);
   return hipGetLastError();
