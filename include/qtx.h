@@ -338,8 +338,9 @@ int32_t qtx_pack_w_ws(const int8_t* W, int32_t N, int32_t K, int8_t* out, void* 
  * column tile; pmax_n <= 128); 3 = fp32 X [M,K] quantized per token from its own row
  * absmax (the scale amode 2 forms from complete partials).  flags: 1 ReLU, 2 residual
  * (res), 4 partial row absmax of the output per 16-column tile into pmax_out [N/16][M].
- * N % 16 == 0, K in {512, 2048} (amode 1: K = 512).  quant_linear.py:111-119,
- * layer_norm.py:12-15. */
+ * N % 16 == 0, K in {512, 2048} (amode 1: K = 512); M * max(ldx, K), M * N and N * K below
+ * 2^30 (the kernels address their operands with 32-bit byte offsets), else QTX_E_UNSUPPORTED.
+ * quant_linear.py:111-119, layer_norm.py:12-15. */
 int32_t qtx_skinny_linear(int32_t amode, const int8_t* A, const float* sa, const float* X,
                           int64_t ldx, const float* ln_a, const float* ln_b,
                           const float* pmax_in, int32_t pmax_n, const void* W, const float* sw,
